@@ -1,0 +1,243 @@
+// C ABI of the EnergyEquivGNN hot path (declared in include/eelg.h) plus the
+// hand-written kernels: edge embedding and the CSR segmented sum.  The
+// irreps-specialised tensor-product and symmetric-contraction kernels are
+// generated into generated/eelg_gen.hip (see gen_kernels.py) and compiled in
+// this same translation unit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/eelg.h"
+#include "eelg_internal.h"
+#include "generated/eelg_gen.hip"
+
+#define EELG_VERSION "eelg 0.1.0 gfx950"
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(-3, "%s: launch failed: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// edge embedding: one thread per edge
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void edge_embed_kernel(
+    const float* __restrict__ pos, const int* __restrict__ sender, const int* __restrict__ receiver,
+    const float* __restrict__ shifts, const float* __restrict__ radius, int n_edges, int lmax,
+    int nb, float len_end, float rad_end, float* __restrict__ sh, float* __restrict__ feats) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_edges) return;
+  const int s = sender[e], r = receiver[e];
+  const float vx = pos[3 * r + 0] - pos[3 * s + 0] + shifts[3 * e + 0];
+  const float vy = pos[3 * r + 1] - pos[3 * s + 1] + shifts[3 * e + 1];
+  const float vz = pos[3 * r + 2] - pos[3 * s + 2] + shifts[3 * e + 2];
+  const float len = sqrtf(vx * vx + vy * vy + vz * vz);
+  const int nsh = (lmax + 1) * (lmax + 1);
+  if (lmax == 4) sh_eval_l4(vx, vy, vz, sh + (size_t)e * nsh);
+  else sh_eval_l3(vx, vy, vz, sh + (size_t)e * nsh);
+  // soft_one_hot_linspace(x, 0, end, nb, 'gaussian', cutoff=False):
+  // values = linspace(0, end, nb); step = values[1]-values[0]; exp(-((x-v)/step)^2)/1.12
+  const float rad = radius[e];
+  const float lstep = len_end / (float)(nb - 1);
+  const float rstep = rad_end / (float)(nb - 1);
+  float* __restrict__ f = feats + (size_t)e * 2 * nb;
+  for (int k = 0; k < nb; ++k) {
+    const float vl = (k == nb - 1) ? len_end : lstep * (float)k;
+    const float vr = (k == nb - 1) ? rad_end : rstep * (float)k;
+    const float dl = (len - vl) / lstep;
+    const float dr = (rad - vr) / rstep;
+    f[k] = expf(-dl * dl) / 1.12f;
+    f[nb + k] = expf(-dr * dr) / 1.12f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSR segmented sum: one wave per output row, float4 over the row when aligned
+// ---------------------------------------------------------------------------
+template <bool VEC4>
+__global__ __launch_bounds__(256) void segment_sum_kernel(
+    const float* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ idx,
+    const float* __restrict__ row_scale, float scale, int n_rows, int width,
+    float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  const float sc = scale * (row_scale ? row_scale[row] : 1.0f);
+  float* __restrict__ o = out + (size_t)row * width;
+  if (VEC4) {
+    const int w4 = width >> 2;
+    for (int c = lane; c < w4; c += 64) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = beg; j < end; ++j) {
+        const int sr = idx ? idx[j] : j;
+        const float4 v = reinterpret_cast<const float4*>(src + (size_t)sr * width)[c];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
+      reinterpret_cast<float4*>(o)[c] = acc;
+    }
+  } else {
+    for (int c = lane; c < width; c += 64) {
+      float acc = 0.f;
+      for (int j = beg; j < end; ++j) {
+        const int sr = idx ? idx[j] : j;
+        acc += src[(size_t)sr * width + c];
+      }
+      o[c] = acc * sc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* eelg_version(void) { return EELG_VERSION; }
+const char* eelg_last_error(void) { return g_err; }
+
+int eelg_tp_find(const char* name) {
+  int n = 0;
+  const eelg_tp_cfg* t = eelg_tp_table(&n);
+  for (int i = 0; i < n; ++i)
+    if (strcmp(t[i].name, name) == 0) return i;
+  return fail(-1, "unknown tensor-product config '%s'", name);
+}
+
+int eelg_tp_info(int cfg, int* info, uint64_t* sig) {
+  int n = 0;
+  const eelg_tp_cfg* t = eelg_tp_table(&n);
+  if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
+  const eelg_tp_cfg& c = t[cfg];
+  info[0] = c.din; info[1] = c.dmid; info[2] = c.wn; info[3] = c.nsh;
+  info[4] = c.ngroups; info[5] = c.npaths; info[6] = c.lmax;
+  *sig = c.sig;
+  return 0;
+}
+
+int eelg_sc_find(const char* name) {
+  int n = 0;
+  const eelg_sc_cfg* t = eelg_sc_table(&n);
+  for (int i = 0; i < n; ++i)
+    if (strcmp(t[i].name, name) == 0) return i;
+  return fail(-1, "unknown symmetric-contraction config '%s'", name);
+}
+
+int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
+  int n = 0;
+  const eelg_sc_cfg* t = eelg_sc_table(&n);
+  if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
+  const eelg_sc_cfg& c = t[cfg];
+  info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
+  *sig = c.sig;
+  return 0;
+}
+
+int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, const float* shifts,
+                    const float* radius, int n_edges, int lmax, int nb, float len_end,
+                    float rad_end, float* sh, float* feats, void* stream) {
+  if (lmax != 3 && lmax != 4) return fail(-2, "edge_embed: lmax %d not built (3 or 4)", lmax);
+  if (nb < 2) return fail(-2, "edge_embed: need >= 2 bases, got %d", nb);
+  if (n_edges <= 0) return 0;
+  hipLaunchKernelGGL(edge_embed_kernel, dim3((n_edges + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, pos, sender, receiver, shifts, radius, n_edges, lmax, nb,
+                     len_end, rad_end, sh, feats);
+  return check_launch("edge_embed");
+}
+
+int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream) {
+  int n = 0;
+  const eelg_tp_cfg* t = eelg_tp_table(&n);
+  if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
+  if (n_nodes <= 0) return 0;
+  const eelg_tp_cfg& c = t[cfg];
+  dim3 grid((n_nodes + 7) / 8, c.ngroups);
+  hipLaunchKernelGGL(c.fwd, grid, dim3(256), 0, (hipStream_t)stream, x, sh, w, sender, rowptr,
+                     n_nodes, inv_norm, agg);
+  return check_launch("tp_fwd");
+}
+
+int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                float* grad_w, float* gxe, void* stream) {
+  int n = 0;
+  const eelg_tp_cfg* t = eelg_tp_table(&n);
+  if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
+  if (n_edges <= 0) return 0;
+  const eelg_tp_cfg& c = t[cfg];
+  hipLaunchKernelGGL(c.bwd, dim3((n_edges + 7) / 8, c.nbgroups), dim3(256), 0, (hipStream_t)stream, x, sh, w,
+                     sender, receiver, n_edges, grad_agg, inv_norm, grad_w, gxe);
+  return check_launch("tp_bwd");
+}
+
+int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
+                         const float* row_scale, float scale, int n_rows, int width, float* out,
+                         void* stream) {
+  if (n_rows <= 0 || width <= 0) return 0;
+  dim3 grid((n_rows + 3) / 4);
+  const bool vec = (width % 4 == 0) && ((uintptr_t)src % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL(segment_sum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, src,
+                       rowptr, idx, row_scale, scale, n_rows, width, out);
+  else
+    hipLaunchKernelGGL(segment_sum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src,
+                       rowptr, idx, row_scale, scale, n_rows, width, out);
+  return check_launch("segment_sum_csr");
+}
+
+static const eelg_sc_cfg* sc_get(int cfg, int mul) {
+  int n = 0;
+  const eelg_sc_cfg* t = eelg_sc_table(&n);
+  if (cfg < 0 || cfg >= n) { fail(-1, "bad sc config %d", cfg); return nullptr; }
+  if (mul != 32) { fail(-2, "symmetric contraction built for mul=32, got %d", mul); return nullptr; }
+  return &t[cfg];
+}
+
+int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
+                void* stream) {
+  const eelg_sc_cfg* c = sc_get(cfg, mul);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->fwd, dim3((n_nodes + 63) / 64, mul / 4), dim3(256), 0,
+                     (hipStream_t)stream, x, coef, n_nodes, out);
+  return check_launch("sc_fwd");
+}
+
+int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
+                  int mul, float* grad_x, void* stream) {
+  const eelg_sc_cfg* c = sc_get(cfg, mul);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->bwd_x, dim3((n_nodes + 63) / 64, mul / 4), dim3(256), 0,
+                     (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x);
+  return check_launch("sc_bwd_x");
+}
+
+int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes, int mul,
+                     int chunk, float* partial, void* stream) {
+  const eelg_sc_cfg* c = sc_get(cfg, mul);
+  if (!c) return -1;
+  if (chunk <= 0) return fail(-2, "sc_bwd_coef: chunk must be > 0");
+  if (n_nodes <= 0) return 0;
+  const int nch = (n_nodes + chunk - 1) / chunk;
+  hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul / 4, c->njg), dim3(256), 0, (hipStream_t)stream, x,
+                     grad_out, n_nodes, chunk, partial);
+  return check_launch("sc_bwd_coef");
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+// Internal declarations shared by the generated and hand-written HIP sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef void (*eelg_tp_fwd_fn)(const float*, const float*, const float*, const int*, const int*, int,
+                               float, float*);
+typedef void (*eelg_tp_bwd_fn)(const float*, const float*, const float*, const int*, const int*, int,
+                               const float*, float, float*, float*);
+typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
+typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*);
+typedef void (*eelg_sc_bwdc_fn)(const float*, const float*, int, int, float*);
+
+struct eelg_tp_cfg {
+  const char* name;
+  int din, dmid, wn, nsh, ngroups, npaths, lmax, nbgroups;
+  uint64_t sig;
+  eelg_tp_fwd_fn fwd;
+  eelg_tp_bwd_fn bwd;
+};
+
+struct eelg_sc_cfg {
+  const char* name;
+  int D, drow, orow, nterms, njg;
+  uint64_t sig;
+  eelg_sc_fwd_fn fwd;
+  eelg_sc_bwdx_fn bwd_x;
+  eelg_sc_bwdc_fn bwd_coef;
+};
+
+const eelg_tp_cfg* eelg_tp_table(int* n);
+const eelg_sc_cfg* eelg_sc_table(int* n);

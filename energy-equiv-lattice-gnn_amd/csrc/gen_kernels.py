@@ -1,0 +1,514 @@
+#!/usr/bin/env python3
+"""Build-time generator for the irreps-specialised HIP kernels (gfx950).
+
+Emits ``generated/eelg_gen.hip``: straight-line, compile-time-indexed code for
+
+* ``sh_eval_l<L>``           real spherical harmonics (recursion constants as literals)
+* ``tp_fwd_<cfg>``           fused gather(x[sender]) -> 'uvu' CG tensor product ->
+                             CSR segmented sum over in-edges -> / agg_norm_const
+* ``tp_bwd_<cfg>``           per-edge grad of the TP weights and per-edge grad of
+                             x[sender] (summed per sender by ``segment_sum_csr``)
+* ``sc_fwd_<cfg>``           symmetric contraction as a sparse cubic polynomial
+                             per (node, channel); coefficients are wave-uniform
+                             (scalar loads), one wave = 64 nodes x 1 channel
+* ``sc_bwd_x_<cfg>``         its gradient w.r.t. the node features
+* ``sc_bwd_coef_<cfg>``      its gradient w.r.t. the per-term coefficients
+                             (per-lane partial sums over nodes, LDS transpose-reduce)
+
+Structure (CG sparsity, term lists, offsets) comes from ``gnn/cg.py``; the
+C-ABI in ``eelg_capi.hip`` exposes each config by name together with a
+structural hash that the Python host re-derives and checks at load time.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+from typing import Dict, List, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from gnn import cg  # noqa: E402
+from gnn.irreps import Ir, Irreps  # noqa: E402
+
+MUL = 32
+
+
+fnv1a64 = cg.fnv1a64
+
+
+def flit(v: float) -> str:
+    r = repr(float(v))
+    if "e" not in r and "." not in r and "inf" not in r and "nan" not in r:
+        r += ".0"
+    return r + "f"
+
+
+# ---------------------------------------------------------------------------
+# configurations
+# ---------------------------------------------------------------------------
+def hidden_irreps(lmax: int, mul: int = MUL) -> Irreps:
+    return Irreps("+".join(f"{mul}x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+
+
+def tp_configs() -> Dict[str, Tuple[Irreps, Irreps, Irreps]]:
+    out = {}
+    for lmax in (3, 4):
+        sh = Irreps.spherical_harmonics(lmax)
+        target = (sh * MUL).sort()[0].simplify()
+        out[f"tpA_l{lmax}"] = (Irreps(f"{MUL}x0e"), sh, target)
+        out[f"tpB_l{lmax}"] = (hidden_irreps(lmax), sh, target)
+    return out
+
+
+def sc_configs() -> Dict[str, Tuple[str, Tuple[int, ...], int]]:
+    out = {}
+    for lmax in (3, 4):
+        coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+        out[f"sc_l{lmax}_c3"] = (coupling, tuple(range(lmax + 1)), 3)
+    return out
+
+
+tp_signature = cg.tp_signature
+sc_signature = cg.sc_signature
+
+
+# ---------------------------------------------------------------------------
+# spherical harmonics
+# ---------------------------------------------------------------------------
+def emit_sh(lmax: int) -> str:
+    L = []
+    L.append(f"// real SH up to l={lmax}, e3nn 'component' normalisation, input need not be unit")
+    L.append(f"__device__ __forceinline__ void sh_eval_l{lmax}(float vx, float vy, float vz, float* __restrict__ out) {{")
+    L.append("  float n = sqrtf(vx * vx + vy * vy + vz * vz);")
+    L.append("  float inv = 1.0f / fmaxf(n, 1e-12f);")
+    L.append("  float v0 = vx * inv, v1 = vy * inv, v2 = vz * inv;")
+    L.append("  float y0_0 = 1.0f;")
+    if lmax >= 1:
+        L.append("  float y1_0 = v0, y1_1 = v1, y1_2 = v2;")
+    for l, terms in enumerate(cg.sh_recursion(lmax), start=1):
+        acc: Dict[int, List[str]] = {}
+        for i, j, k, c in terms:
+            acc.setdefault(k, []).append(f"{flit(c)} * y{l}_{i} * v{j}")
+        for k in range(2 * l + 3):
+            expr = " + ".join(acc.get(k, ["0.0f"]))
+            L.append(f"  float y{l + 1}_{k} = {expr};")
+    idx = 0
+    for l in range(lmax + 1):
+        s = math.sqrt(2 * l + 1)
+        for m in range(2 * l + 1):
+            L.append(f"  out[{idx}] = {flit(s)} * y{l}_{m};")
+            idx += 1
+    L.append("}")
+    return "\n".join(L)
+
+
+# ---------------------------------------------------------------------------
+# tensor product
+# ---------------------------------------------------------------------------
+def _path_cg(p: cg.TPPath):
+    return cg.nonzeros(cg.wigner_3j(p.l1, p.l2, p.l3))
+
+
+def _group_paths(paths: List[cg.TPPath], max_acc: int) -> List[List[cg.TPPath]]:
+    """Contiguous groups (slot order) with <= max_acc accumulators per lane."""
+    groups, cur, n = [], [], 0
+    for p in paths:
+        d = 2 * p.l3 + 1
+        if cur and n + d > max_acc:
+            groups.append(cur)
+            cur, n = [], 0
+        cur.append(p)
+        n += d
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+def _emit_t(p: cg.TPPath, xname, yname, tname, L: List[str], ind: str):
+    """t_k = sum_{ij} C_ijk x_i y_j for one path; picks the cheaper of
+    pair-products-first and M-first (M_ik = sum_j C_ijk y_j)."""
+    nz = _path_cg(p)
+    pairs = sorted({(i, j) for (i, j, k), _ in nz})
+    iks = sorted({(i, k) for (i, j, k), _ in nz})
+    d3 = 2 * p.l3 + 1
+    terms_by_k: Dict[int, List] = {k: [] for k in range(d3)}
+    if len(pairs) <= len(iks):
+        for i, j in pairs:
+            L.append(f"{ind}const float z{i}_{j} = {xname(p, i)} * {yname(p, j)};")
+        for (i, j, k), c in nz:
+            terms_by_k[k].append(f"{flit(c)} * z{i}_{j}")
+    else:
+        byik: Dict[Tuple[int, int], List[str]] = {}
+        for (i, j, k), c in nz:
+            byik.setdefault((i, k), []).append(f"{flit(c)} * {yname(p, j)}")
+        for (i, k), ts in byik.items():
+            L.append(f"{ind}const float m{i}_{k} = {' + '.join(ts)};")
+            terms_by_k[k].append(f"{xname(p, i)} * m{i}_{k}")
+    for k in range(d3):
+        expr = " + ".join(terms_by_k[k]) if terms_by_k[k] else "0.0f"
+        L.append(f"{ind}const float {tname}{k} = {expr};")
+
+
+def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, dict]:
+    paths = cg.tp_paths(node, sh, target)
+    din, nsh = node.dim, sh.dim
+    irreps_mid = cg.tp_out_irreps_with_instructions(node, sh, target)[0]
+    dmid = irreps_mid.dim
+    wn = sum(p.mul for p in paths)
+    for p in paths:
+        assert p.mul == MUL
+    groups = _group_paths(paths, 48)
+    node_ls = [ir.l for _, ir in node]
+    node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
+    L: List[str] = []
+    L.append(f"// ===== tensor product config {name}: {node} (x) {sh} -> {irreps_mid} =====")
+    L.append(f"// {len(paths)} 'uvu' paths, weight_numel {wn}, {len(groups)} path groups")
+    xname = lambda p, i: f"x{p.l1}_{i}"  # noqa: E731
+    yname = lambda p, j: f"y{p.l2 * p.l2 + j}"  # noqa: E731
+
+    # ---------------- forward ----------------
+    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append("  const int lane = threadIdx.x & 63;")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append("  const int node = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
+    L.append("  if (node >= n_nodes) return;")
+    L.append("  const int beg = rowptr[node], end = rowptr[node + 1];")
+    L.append("  float* __restrict__ o = agg + (size_t)node * " + str(dmid) + ";")
+    L.append("  switch (blockIdx.y) {")
+    for gi, grp in enumerate(groups):
+        L.append(f"  case {gi}: {{")
+        need_l1 = sorted({p.l1 for p in grp})
+        need_l2 = sorted({p.l2 for p in grp})
+        for p in grp:
+            for k in range(2 * p.l3 + 1):
+                L.append(f"    float a{p.slot}_{k} = 0.0f;")
+        L.append("    for (int e = beg; e < end; ++e) {")
+        L.append("      const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
+        L.append("      const float* __restrict__ ye = sh + (size_t)e * " + str(nsh) + ";")
+        L.append("      const float* __restrict__ we = w + (size_t)e * " + str(wn) + " + u;")
+        for l in need_l1:
+            d = 2 * l + 1
+            for i in range(d):
+                L.append(f"      const float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
+        for l in need_l2:
+            for j in range(2 * l + 1):
+                L.append(f"      const float y{l * l + j} = ye[{l * l + j}];")
+        for p in grp:
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float wp = we[{p.slot * MUL}] * ({flit(p.coef)} * inv_norm);")
+            _emit_t(p, xname, yname, "t", L, "        ")
+            for k in range(2 * p.l3 + 1):
+                L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+            L.append("      }")
+        L.append("    }")
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            for k in range(d3):
+                L.append(f"    o[{p.out_off} + u * {d3} + {k}] = a{p.slot}_{k};")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+
+    # ---------------- backward (per edge) ----------------
+    # grouped by input block l1: each group owns a disjoint slice of gxe, so no
+    # cross-group reduction is needed; grad_w of every path is written once.
+    bgroups = [[p for p in paths if p.l1 == l] for l in node_ls]
+    bgroups = [g for g in bgroups if g]
+    L.append(f"__global__ __launch_bounds__(256) void tp_bwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ receiver, int n_edges,")
+    L.append("    const float* __restrict__ gagg, float inv_norm,")
+    L.append("    float* __restrict__ gw, float* __restrict__ gxe) {")
+    L.append("  const int lane = threadIdx.x & 63;")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append("  const int e = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
+    L.append("  if (e >= n_edges) return;")
+    L.append("  const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
+    L.append("  const float* __restrict__ ye = sh + (size_t)e * " + str(nsh) + ";")
+    L.append("  const float* __restrict__ we = w + (size_t)e * " + str(wn) + " + u;")
+    L.append("  float* __restrict__ gwe = gw + (size_t)e * " + str(wn) + " + u;")
+    L.append("  const float* __restrict__ ge = gagg + (size_t)receiver[e] * " + str(dmid) + ";")
+    L.append("  float* __restrict__ gxo = gxe + (size_t)e * " + str(din) + ";")
+    L.append("  switch (blockIdx.y) {")
+    for gi, grp in enumerate(bgroups):
+        l = grp[0].l1
+        d = 2 * l + 1
+        L.append(f"  case {gi}: {{ // input block l1 = {l}")
+        for i in range(d):
+            L.append(f"    const float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
+            L.append(f"    float gx{l}_{i} = 0.0f;")
+        for l2 in sorted({p.l2 for p in grp}):
+            for j in range(2 * l2 + 1):
+                L.append(f"    const float y{l2 * l2 + j} = ye[{l2 * l2 + j}];")
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            d1 = 2 * p.l1 + 1
+            L.append(f"    {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"      const float cp = {flit(p.coef)} * inv_norm;")
+            for k in range(d3):
+                L.append(f"      const float g{k} = ge[{p.out_off} + u * {d3} + {k}];")
+            nz = _path_cg(p)
+            byik: Dict[Tuple[int, int], List[str]] = {}
+            for (i, j, k), c in nz:
+                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
+            for (i, k), ts in byik.items():
+                L.append(f"      const float m{i}_{k} = {' + '.join(ts)};")
+            gterms = []
+            for k in range(d3):
+                ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
+                if ts:
+                    gterms.append(f"g{k} * ({' + '.join(ts)})")
+            L.append(f"      gwe[{p.slot * MUL}] = cp * ({' + '.join(gterms) if gterms else '0.0f'});")
+            L.append(f"      const float hw = cp * we[{p.slot * MUL}];")
+            for i in range(d1):
+                ts = [f"m{i}_{k} * g{k}" for k in range(d3) if (i, k) in byik]
+                if ts:
+                    L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
+            L.append("    }")
+        for i in range(d):
+            L.append(f"    gxo[{node_off[l]} + u * {d} + {i}] = gx{l}_{i};")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
+                npaths=len(paths),
+                sig=fnv1a64(tp_signature(node, sh, target)))
+    return "\n".join(L), info
+
+
+# ---------------------------------------------------------------------------
+# symmetric contraction
+# ---------------------------------------------------------------------------
+def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
+    plan = cg.symcon_plan(coupling, ls, corr)
+    irs = [ir for _, ir in Irreps(coupling)]
+    D = sum(ir.dim for ir in irs)
+    # per-component (l, m) of the 25-vector and its offset in the mul-major row
+    comp = []
+    off = 0
+    for ir in irs:
+        for m in range(ir.dim):
+            comp.append((ir.l, m, off))
+        off += MUL * ir.dim
+    drow = off                                   # row width of x (= MUL * D)
+    ocomp = []
+    off = 0
+    for l in ls:
+        for m in range(2 * l + 1):
+            ocomp.append((l, m, off))
+        off += MUL * (2 * l + 1)
+    orow = off
+    nt = len(plan.terms)
+
+    def xaddr(a):
+        l, m, o = comp[a]
+        return f"{o} + c * {2 * l + 1} + {m}"
+
+    def oaddr(q):
+        l, m, o = ocomp[q]
+        return f"{o} + c * {2 * l + 1} + {m}"
+
+    L: List[str] = []
+    L.append(f"// ===== symmetric contraction config {name}: coupling {coupling}, correlation {corr} =====")
+    L.append(f"// {nt} polynomial terms per channel; x row {drow} floats, out row {orow} floats")
+
+    # group terms by (a, b) pair
+    pairs: Dict[Tuple[int, int], Dict] = {}
+    deg1 = []
+    for t, (nu, (a, b, c), q) in enumerate(plan.terms):
+        if nu == 1:
+            deg1.append((t, a, q))
+        else:
+            g = pairs.setdefault((a, b), {"d2": [], "d3": {}})
+            if nu == 2:
+                g["d2"].append((t, q))
+            else:
+                g["d3"].setdefault(c, []).append((t, q))
+
+    # ---------------- forward ----------------
+    L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
+    L.append("    float* __restrict__ out) {")
+    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));")
+    L.append("  const int n = blockIdx.x * 64 + (threadIdx.x & 63);")
+    L.append(f"  const float* __restrict__ cf = coef + (size_t)c * {nt};")
+    L.append("  if (n >= n_nodes) return;")
+    L.append(f"  const float* __restrict__ xr = x + (size_t)n * {drow};")
+    for a in range(D):
+        L.append(f"  const float x{a} = xr[{xaddr(a)}];")
+    for q in range(len(ocomp)):
+        L.append(f"  float o{q} = 0.0f;")
+    for t, a, q in deg1:
+        L.append(f"  o{q} = fmaf(cf[{t}], x{a}, o{q});")
+    for (a, b), g in pairs.items():
+        L.append(f"  {{ const float p = x{a} * x{b};")
+        for t, q in g["d2"]:
+            L.append(f"    o{q} = fmaf(cf[{t}], p, o{q});")
+        for cc, lst in g["d3"].items():
+            L.append(f"    {{ const float m = p * x{cc};")
+            for t, q in lst:
+                L.append(f"      o{q} = fmaf(cf[{t}], m, o{q});")
+            L.append("    }")
+        L.append("  }")
+    L.append(f"  float* __restrict__ orow = out + (size_t)n * {orow};")
+    for q in range(len(ocomp)):
+        L.append(f"  orow[{oaddr(q)}] = o{q};")
+    L.append("}")
+
+    # ---------------- backward w.r.t. x ----------------
+    L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
+    L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx) {")
+    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));")
+    L.append("  const int n = blockIdx.x * 64 + (threadIdx.x & 63);")
+    L.append(f"  const float* __restrict__ cf = coef + (size_t)c * {nt};")
+    L.append("  if (n >= n_nodes) return;")
+    L.append(f"  const float* __restrict__ xr = x + (size_t)n * {drow};")
+    L.append(f"  const float* __restrict__ gr = gout + (size_t)n * {orow};")
+    for a in range(D):
+        L.append(f"  const float x{a} = xr[{xaddr(a)}];")
+        L.append(f"  float d{a} = 0.0f;")
+    for q in range(len(ocomp)):
+        L.append(f"  const float g{q} = gr[{oaddr(q)}];")
+    for t, a, q in deg1:
+        L.append(f"  d{a} = fmaf(cf[{t}], g{q}, d{a});")
+    for (a, b), g in pairs.items():
+        L.append(f"  {{ const float p = x{a} * x{b}; float s2 = 0.0f;")
+        for t, q in g["d2"]:
+            L.append(f"    s2 = fmaf(cf[{t}], g{q}, s2);")
+        for cc, lst in g["d3"].items():
+            L.append("    { float s = 0.0f;")
+            for t, q in lst:
+                L.append(f"      s = fmaf(cf[{t}], g{q}, s);")
+            L.append(f"      d{cc} = fmaf(s, p, d{cc}); s2 = fmaf(s, x{cc}, s2); }}")
+        L.append(f"    d{a} = fmaf(s2, x{b}, d{a}); d{b} = fmaf(s2, x{a}, d{b}); }}")
+    L.append(f"  float* __restrict__ gxr = gx + (size_t)n * {drow};")
+    for a in range(D):
+        L.append(f"  gxr[{xaddr(a)}] = d{a};")
+    L.append("}")
+
+    # ---------------- backward w.r.t. coefficients ----------------
+    JG = 128
+    groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
+    L.append(f"// coefficient gradient: {len(groups)} term groups of <= {JG}; each wave = 1 channel x 64 lanes,")
+    L.append("// lanes walk the nodes of one chunk and keep per-term partial sums in registers,")
+    L.append("// reduced over lanes through an LDS transpose at the end.")
+    L.append(f"__global__ __launch_bounds__(256) void sc_bwd_coef_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ gout, int n_nodes, int chunk,")
+    L.append("    float* __restrict__ part) {")
+    L.append("  __shared__ float red[4][64 * 33];")
+    L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
+    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + wv);")
+    L.append("  const int n0 = blockIdx.x * chunk;")
+    L.append("  const int n1 = min(n_nodes, n0 + chunk);")
+    L.append(f"  float* __restrict__ dst = part + ((size_t)blockIdx.x * {MUL} + c) * {nt};")
+    L.append("  float* __restrict__ r = red[wv];")
+    L.append("  switch (blockIdx.z) {")
+    for gi, grp in enumerate(groups):
+        L.append(f"  case {gi}: {{")
+        need_x, need_g = set(), set()
+        for t in grp:
+            nu, (a, b, cc), q = plan.terms[t]
+            need_g.add(q)
+            need_x.add(a)
+            if nu >= 2:
+                need_x.add(b)
+            if nu >= 3:
+                need_x.add(cc)
+        for t in grp:
+            L.append(f"    float s{t} = 0.0f;")
+        L.append("    for (int n = n0 + lane; n < n1; n += 64) {")
+        L.append(f"      const float* __restrict__ xr = x + (size_t)n * {drow};")
+        L.append(f"      const float* __restrict__ gr = gout + (size_t)n * {orow};")
+        for a in sorted(need_x):
+            L.append(f"      const float x{a} = xr[{xaddr(a)}];")
+        for q in sorted(need_g):
+            L.append(f"      const float g{q} = gr[{oaddr(q)}];")
+        cur_pair = None
+        for t in grp:
+            nu, (a, b, cc), q = plan.terms[t]
+            if nu == 1:
+                L.append(f"      s{t} = fmaf(x{a}, g{q}, s{t});")
+                continue
+            if cur_pair != (a, b):
+                if cur_pair is not None:
+                    L.append("      }")
+                L.append(f"      {{ const float p = x{a} * x{b};")
+                cur_pair = (a, b)
+            if nu == 2:
+                L.append(f"        s{t} = fmaf(p, g{q}, s{t});")
+            else:
+                L.append(f"        s{t} = fmaf(p * x{cc}, g{q}, s{t});")
+        if cur_pair is not None:
+            L.append("      }")
+        L.append("    }")
+        # transpose-reduce in chunks of 32 terms
+        for s0 in range(0, len(grp), 32):
+            sub = grp[s0: s0 + 32]
+            for jj, t in enumerate(sub):
+                L.append(f"    r[lane * 33 + {jj}] = s{t};")
+            L.append("    __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_wave_barrier();")
+            L.append("    { float acc = 0.0f; const int col = lane & 31, half = lane >> 5;")
+            L.append("      #pragma unroll")
+            L.append("      for (int rr = 0; rr < 32; ++rr) acc += r[(half * 32 + rr) * 33 + col];")
+            L.append("      acc += __shfl_xor(acc, 32);")
+            L.append(f"      if (lane < {len(sub)}) dst[{grp[s0]} + lane] = acc; }}")
+            L.append("    __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_wave_barrier();")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    info = dict(D=D, drow=drow, orow=orow, nterms=nt, njg=len(groups),
+                sig=fnv1a64(sc_signature(coupling, ls, corr)))
+    return "\n".join(L), info
+
+
+# ---------------------------------------------------------------------------
+def main(outdir: str) -> None:
+    os.makedirs(outdir, exist_ok=True)
+    parts = ["// GENERATED by csrc/gen_kernels.py -- do not edit", "#include <hip/hip_runtime.h>",
+             "#include <stdint.h>", '#include "../eelg_internal.h"', ""]
+    for lmax in (3, 4):
+        parts.append(emit_sh(lmax))
+    tp_table, sc_table = [], []
+    for name, (node, sh, target) in tp_configs().items():
+        code, info = emit_tp(name, node, sh, target)
+        parts.append(code)
+        tp_table.append((name, info))
+    for name, (coupling, ls, corr) in sc_configs().items():
+        code, info = emit_sc(name, coupling, ls, corr)
+        parts.append(code)
+        sc_table.append((name, info))
+    # launch tables
+    parts.append("\n// ===== config tables =====")
+    parts.append("static const eelg_tp_cfg kTpConfigs[] = {")
+    for name, i in tp_table:
+        lmax = int(name.split("_l")[1])
+        parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
+                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}}},')
+    parts.append("};")
+    parts.append("static const eelg_sc_cfg kScConfigs[] = {")
+    for name, i in sc_table:
+        parts.append(f'  {{"{name}", {i["D"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, '
+                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}}},')
+    parts.append("};")
+    parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
+    parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")
+    src = "\n".join(parts) + "\n"
+    path = os.path.join(outdir, "eelg_gen.hip")
+    old = open(path).read() if os.path.exists(path) else None
+    if old != src:
+        with open(path, "w") as f:
+            f.write(src)
+    print(f"wrote {path}: {len(src.splitlines())} lines")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "generated"))

@@ -1,0 +1,100 @@
+"""ctypes binding of ``libeelg.so`` (C ABI declared in ``include/eelg.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` /
+``make -C energy-equiv-lattice-gnn_amd/csrc``.  There is no fallback: if the
+library is missing or stale every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Tuple
+
+import torch  # noqa: F401  (loads torch's libamdhip64 first; the .so binds to it by SONAME)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeelg.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+_SIGS = {
+    "eelg_version": ([], ctypes.c_char_p),
+    "eelg_last_error": ([], ctypes.c_char_p),
+    "eelg_tp_find": ([ctypes.c_char_p], _I),
+    "eelg_tp_info": ([_I, _P, _P], _I),
+    "eelg_sc_find": ([ctypes.c_char_p], _I),
+    "eelg_sc_info": ([_I, _P, _P], _I),
+    "eelg_edge_embed": ([_P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _P, _P, _P], _I),
+    "eelg_tp_fwd": ([_I, _P, _P, _P, _P, _P, _I, _F, _P, _P], _I),
+    "eelg_tp_bwd": ([_I, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
+    "eelg_segment_sum_csr": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
+    "eelg_sc_fwd": ([_I, _P, _P, _I, _I, _P, _P], _I),
+    "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),
+    "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+class EELGError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EELGError(
+            f"{LIB_PATH} is missing: build it with `python -c \"import __graft_entry__ as g; g.build()\"` "
+            "(there is no CPU fallback for the HIP hot path)")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().eelg_last_error().decode(errors="replace")
+        raise EELGError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> ctypes.c_void_p:
+    if t is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def tp_config(name: str) -> Tuple[int, Dict[str, int], int]:
+    lib = load()
+    idx = lib.eelg_tp_find(name.encode())
+    if idx < 0:
+        check(idx, f"tp config {name}")
+    info = (ctypes.c_int * 7)()
+    sig = ctypes.c_uint64()
+    check(lib.eelg_tp_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P)), "tp_info")
+    keys = ("din", "dmid", "wn", "nsh", "ngroups", "npaths", "lmax")
+    return idx, dict(zip(keys, list(info))), sig.value
+
+
+def sc_config(name: str) -> Tuple[int, Dict[str, int], int]:
+    lib = load()
+    idx = lib.eelg_sc_find(name.encode())
+    if idx < 0:
+        check(idx, f"sc config {name}")
+    info = (ctypes.c_int * 5)()
+    sig = ctypes.c_uint64()
+    check(lib.eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P)), "sc_info")
+    keys = ("D", "x_row", "out_row", "nterms", "njg")
+    return idx, dict(zip(keys, list(info))), sig.value

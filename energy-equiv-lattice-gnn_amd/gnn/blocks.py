@@ -1,0 +1,222 @@
+"""Hot-path blocks of the reference ``gnn/blocks.py``, MI355X-native.
+
+Constructors, module names, parameter names and ``forward`` signatures follow
+the reference, so ``state_dict``s round-trip (the reference's large
+``U_matrix_*`` buffers are derived data and are not stored here).
+
+``edge_index`` arguments accept either the reference's ``[2, E]`` tensor (the
+edge tensors are then in the caller's order and get permuted once) or an
+``ops.EdgeCSR`` (edge tensors already in receiver-sorted order, the fast path
+used by ``EnergyEquivGNN``).
+"""
+from __future__ import annotations
+
+from argparse import Namespace
+from typing import Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib, cg, ops
+from .irreps import Irreps
+from .mace import SymmetricContraction
+from .o3 import Gate, Linear, TensorProduct
+
+EdgeIndex = Union[torch.Tensor, ops.EdgeCSR]
+
+
+def as_csr(edge_index: EdgeIndex, num_nodes: int, *edge_tensors):
+    """Returns (csr, edge tensors in csr order)."""
+    if isinstance(edge_index, ops.EdgeCSR):
+        return (edge_index,) + tuple(edge_tensors)
+    csr = ops.EdgeCSR.build(edge_index, num_nodes)
+    return (csr,) + tuple(t[csr.perm] for t in edge_tensors)
+
+
+class PositiveLayer(torch.nn.Module):
+    """``gnn/blocks.py:185-229``."""
+
+    def __init__(self, params: Namespace):
+        super().__init__()
+        f = params.positive_function
+        eye = lambda c: torch.eye(6, device=c.device, dtype=c.dtype)  # noqa: E731
+        funcs = {
+            "matrix_power_2": lambda c: torch.linalg.matrix_power(c, 2),
+            "matrix_power_4": lambda c: torch.linalg.matrix_power(c, 4),
+            "matrix_exp": torch.linalg.matrix_exp,
+            "matrix_trunc_exp_2": lambda c: torch.linalg.matrix_power(eye(c) + c / 2, 2),
+            "matrix_trunc_exp_4": lambda c: torch.linalg.matrix_power(eye(c) + c / 4, 4),
+            "none": lambda c: c,
+        }
+        if f not in funcs:
+            raise ValueError(f"Unknown positive function: {f}")
+        self.func = funcs[f]
+
+    def forward(self, c):
+        return self.func(c)
+
+
+class GeneralNonLinearReadoutBlock(torch.nn.Module):
+    """``gnn/blocks.py:250-283``."""
+
+    def __init__(self, irreps_in, hidden_irreps, irreps_out, gate=None):
+        super().__init__()
+        hidden_irreps, irreps_out = Irreps(hidden_irreps), Irreps(irreps_out)
+        self.hidden_irreps, self.irreps_out = hidden_irreps, irreps_out
+        scal = Irreps([(m, ir) for m, ir in hidden_irreps if ir.l == 0 and ir in irreps_out])
+        gated = Irreps([(m, ir) for m, ir in hidden_irreps if ir.l > 0 and ir in irreps_out])
+        gates = Irreps([(m, "0e") for m, _ in gated])
+        self.equivariant_nonlin = Gate(scal, gates, gated)
+        self.irreps_nonlin = self.equivariant_nonlin.irreps_in.simplify()
+        self.linear_1 = Linear(irreps_in, self.irreps_nonlin)
+        self.linear_2 = Linear(self.equivariant_nonlin.irreps_out, irreps_out)
+
+    def forward(self, x):
+        return self.linear_2(self.equivariant_nonlin(self.linear_1(x)))
+
+
+class Cart_4_to_Mandel(torch.nn.Module):  # noqa: N801
+    """``gnn/blocks.py:392-425``: a fixed linear map 81 -> 36 applied as one GEMM."""
+
+    a = [0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 1, 1, 1, 0, 0, 0]
+    b = [0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1]
+    c = [0, 1, 2, 1, 0, 0, 1, 2, 1, 0, 0, 2, 1, 0, 0, 1, 0, 0, 0, 0, 0]
+    d = [0, 1, 2, 2, 2, 1, 1, 2, 2, 2, 1, 2, 2, 2, 1, 2, 2, 1, 2, 1, 1]
+
+    def __init__(self):
+        super().__init__()
+        s2 = np.sqrt(2)
+        mask = np.array([[1, 1, 1, s2, s2, s2]] * 3 + [[s2, s2, s2, 2, 2, 2]] * 3)
+        rows, cols = np.triu_indices(6)
+        m = np.zeros((81, 36))
+        for t, (r, q) in enumerate(zip(rows, cols)):
+            src = ((self.a[t] * 3 + self.b[t]) * 3 + self.c[t]) * 3 + self.d[t]
+            m[src, r * 6 + q] = mask[r, q]
+            m[src, q * 6 + r] = mask[q, r]
+        self.register_buffer("map", torch.tensor(m, dtype=torch.float32), persistent=False)
+
+    def forward(self, c):
+        return (c.reshape(c.shape[0], 81) @ self.map).view(c.shape[0], 6, 6)
+
+
+class Spherical_to_Cartesian(torch.nn.Module):  # noqa: N801
+    """``gnn/blocks.py:427-442`` with the change of basis of ``cg.stiffness_change_of_basis``."""
+
+    def __init__(self):
+        super().__init__()
+        q = torch.tensor(cg.stiffness_change_of_basis(), dtype=torch.float32)
+        self.register_buffer("Q_flat", q.reshape(21, 81))
+
+    def forward(self, x):
+        return (x @ self.Q_flat).view(*x.shape[:-1], 3, 3, 3, 3)
+
+
+class EquivariantProductBlock(torch.nn.Module):
+    """``gnn/blocks.py:447-490``."""
+
+    def __init__(self, node_feats_irreps, target_irreps, correlation: int, use_sc: bool = True):
+        super().__init__()
+        node_feats_irreps = Irreps(node_feats_irreps)
+        self.use_sc = use_sc
+        mul = node_feats_irreps.count("0e")
+        sc_out = Irreps([(mul, ir) for _, ir in Irreps(target_irreps)])
+        self.symmetric_contractions = SymmetricContraction(node_feats_irreps, sc_out, correlation)
+        self.linear = Linear(sc_out, target_irreps)
+
+    def forward(self, node_feats, sc):
+        x = self.linear(self.symmetric_contractions(node_feats))
+        return x + sc if self.use_sc else x
+
+
+class TensorProductInteractionBlock(torch.nn.Module):
+    """``gnn/blocks.py:495-604`` with ``conv_tp`` + ``scatter / agg_norm_const`` fused
+    into one HIP kernel (``eelg_tp_fwd``)."""
+
+    def __init__(self, node_feats_irreps, edge_attrs_irreps, edge_feats_irreps, irreps_out,
+                 agg_norm_const, reduce: str = "sum", bias: bool = False, MLP_dim: int = 64,
+                 MLP_layers: int = 3):
+        super().__init__()
+        self._node_feats_irreps = Irreps(node_feats_irreps)
+        self.edge_attrs_irreps = Irreps(edge_attrs_irreps)
+        self.edge_feats_irreps = Irreps(edge_feats_irreps)
+        self._irreps_out = Irreps(irreps_out)
+        self.agg_norm_const = float(agg_norm_const)
+        self.reduce = reduce.lower()
+        if self.reduce != "sum":
+            raise NotImplementedError("only interaction_reduction='sum' is on the hot path "
+                                      "(the PNA branch is out of scope, SURVEY.md section 2)")
+        self.linear_up = Linear(self._node_feats_irreps, self._node_feats_irreps)
+        irreps_mid, instructions = cg.tp_out_irreps_with_instructions(
+            self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
+        self.conv_tp = TensorProduct(self._node_feats_irreps, self.edge_attrs_irreps, irreps_mid,
+                                     instructions)
+        layer = torch.nn.Linear(MLP_dim, self.conv_tp.weight_numel, bias=False)
+        torch.nn.init.xavier_uniform_(layer.weight, gain=10)
+        self.conv_tp_weights = torch.nn.Sequential(
+            torch.nn.Linear(self.edge_feats_irreps.num_irreps, MLP_dim), torch.nn.SiLU())
+        for _ in range(MLP_layers - 2):
+            self.conv_tp_weights.append(torch.nn.Linear(MLP_dim, MLP_dim))
+            self.conv_tp_weights.append(torch.nn.SiLU())
+        self.conv_tp_weights.append(layer)
+        self.irreps_mid = irreps_mid.simplify()
+        self.linear = Linear(self.irreps_mid, self._irreps_out, biases=bias)
+        # which generated kernel set serves this block
+        lmax = self.edge_attrs_irreps.lmax
+        hidden = Irreps("+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+        if self._node_feats_irreps == Irreps("32x0e"):
+            self.cfg_name = f"tpA_l{lmax}"
+        elif self._node_feats_irreps == hidden:
+            self.cfg_name = f"tpB_l{lmax}"
+        else:
+            raise NotImplementedError(f"no generated tensor-product kernel for node irreps "
+                                      f"{self._node_feats_irreps} with SH lmax {lmax}")
+        self._sig = cg.fnv1a64(cg.tp_signature(self._node_feats_irreps, self.edge_attrs_irreps,
+                                               self._irreps_out))
+        self._cfg = None
+
+    @property
+    def irreps_in(self):
+        return self._node_feats_irreps
+
+    @property
+    def irreps_out(self):
+        return self._irreps_out
+
+    def _config(self):
+        if self._cfg is None:
+            idx, info, sig = _lib.tp_config(self.cfg_name)
+            if sig != self._sig:
+                raise _lib.EELGError(f"libeelg.so was built for a different {self.cfg_name} "
+                                     "structure; rebuild it")
+            self._cfg = (idx, info)
+        return self._cfg
+
+    def forward(self, node_feats, edge_attrs, edge_feats, edge_index: EdgeIndex,
+                node_attrs: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, None]:
+        csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
+        idx, info = self._config()
+        x = self.linear_up(node_feats)
+        w = self.conv_tp_weights(edge_feats)
+        agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
+        return self.linear(agg), None
+
+
+class MACELayer(torch.nn.Module):
+    """``gnn/blocks.py:902-947``."""
+
+    def __init__(self, input_irreps, edge_sh_irreps, edge_scalars_irreps, interaction_irreps,
+                 output_irreps, interaction_agg_norm_const, interaction_reduction: str,
+                 interaction_bias: bool, product_correlation: int, MLP_dim: int = 64,
+                 MLP_layers: int = 3):
+        super().__init__()
+        self.interaction = TensorProductInteractionBlock(
+            input_irreps, edge_sh_irreps, edge_scalars_irreps, interaction_irreps,
+            interaction_agg_norm_const, interaction_reduction, interaction_bias, MLP_dim,
+            MLP_layers)
+        self.product = EquivariantProductBlock(self.interaction.irreps_out, output_irreps,
+                                               product_correlation, use_sc=False)
+
+    def forward(self, node_ft, edge_index: EdgeIndex, edge_sh, edge_scalars):
+        csr, edge_sh, edge_scalars = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_scalars)
+        node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr)
+        return self.product(node_ft, sc)

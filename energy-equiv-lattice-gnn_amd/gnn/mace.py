@@ -1,0 +1,88 @@
+"""MACE-derived pieces of the hot path (reference ``gnn/mace.py``).
+
+``SymmetricContraction`` keeps the reference's module/parameter layout
+(``contractions['32x0e'].weights['1'|'2'|'3']`` with shapes ``[K_nu, mul]``,
+``gnn/mace.py:112-240``) but evaluates the contraction as the sparse
+symmetrised polynomial of ``gnn/cg.py:symcon_plan``: the per-term coefficients
+``coef[c, t] = (U_sym @ W)[t, c]`` are one small GEMM per call, and the
+polynomial itself runs in the generated HIP kernels (``sc_fwd/bwd_*``).  The
+dense ``[N, 32, 2l+1, 25, 25]`` intermediate of the reference never exists.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, cg, ops
+from .irreps import Ir, Irreps
+
+tp_out_irreps_with_instructions = cg.tp_out_irreps_with_instructions
+
+
+def get_edge_vectors_and_lengths(positions, edge_index, shifts):
+    """``gnn/mace.py:338-352`` (normalize=False); the model itself uses the fused
+    ``eelg_edge_embed`` kernel."""
+    sender, receiver = edge_index
+    vectors = positions[receiver] - positions[sender] + shifts
+    return vectors, torch.linalg.norm(vectors, dim=-1, keepdim=True)
+
+
+class Contraction(torch.nn.Module):
+    """Parameter holder with the reference's names (``gnn/mace.py:230-238``)."""
+
+    def __init__(self, ks, num_features: int):
+        super().__init__()
+        self.weights = torch.nn.ParameterDict(
+            {str(nu): torch.nn.Parameter(torch.randn(k, num_features) / k)
+             for nu, k in enumerate(ks, start=1)})
+
+
+class SymmetricContraction(torch.nn.Module):
+    def __init__(self, irreps_in, irreps_out, correlation: int):
+        super().__init__()
+        self.irreps_in, self.irreps_out = Irreps(irreps_in), Irreps(irreps_out)
+        self.mul = self.irreps_in.count("0e")
+        self.correlation = correlation
+        coupling = "+".join(str(ir) for _, ir in self.irreps_in)
+        lmax = self.irreps_in.lmax
+        ls = tuple(ir.l for _, ir in self.irreps_out)
+        expect = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+        if (coupling != expect or ls != tuple(range(lmax + 1)) or correlation != 3
+                or any(m != self.mul for m, _ in self.irreps_in) or self.mul != 32):
+            raise NotImplementedError(
+                f"symmetric contraction kernels are generated for 32x(0e..{lmax}) in/out, "
+                f"correlation 3; got {self.irreps_in} -> {self.irreps_out}, correlation {correlation}")
+        self.cfg_name = f"sc_l{lmax}_c{correlation}"
+        plan = cg.symcon_plan(coupling, ls, correlation)
+        self._sig = cg.fnv1a64(cg.sc_signature(coupling, ls, correlation))
+        self.block_order = [(l, nu) for l, nu, _ in plan.weight_blocks]
+        ks = {}
+        for l, nu, k in plan.weight_blocks:
+            ks.setdefault(l, []).append(k)
+        self.contractions = torch.nn.ModuleDict()
+        for mul, ir in self.irreps_out:
+            self.contractions[f"{mul}x{ir}"] = Contraction(ks[ir.l], self.mul)
+        self.register_buffer("u_sym", torch.tensor(plan.ubig, dtype=torch.float32), persistent=False)
+        self._cfg = None
+
+    def _config(self):
+        if self._cfg is None:
+            idx, info, sig = _lib.sc_config(self.cfg_name)
+            if sig != self._sig:
+                raise _lib.EELGError(f"libeelg.so was built for a different {self.cfg_name} "
+                                     "structure; rebuild it")
+            self._cfg = (idx, info)
+        return self._cfg
+
+    def weight_matrix(self) -> torch.Tensor:
+        ws = []
+        for l, nu in self.block_order:
+            ir = Ir(l, (-1) ** l)
+            ws.append(self.contractions[f"{self.mul}x{ir}"].weights[str(nu)])
+        return torch.cat(ws, dim=0)                     # [K_total, mul]
+
+    def coefficients(self) -> torch.Tensor:
+        return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()   # [mul, nterms]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        idx, info = self._config()
+        return ops.symmetric_contraction(x, self.coefficients(), idx, info, self.mul)

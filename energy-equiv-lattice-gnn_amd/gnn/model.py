@@ -1,0 +1,110 @@
+"""``GNN_Head`` / ``EnergyEquivGNN`` (reference ``gnn/model.py:26-161``), MI355X-native.
+
+Same constructor (``params`` Namespace), module tree, parameter names and
+``forward(batch) -> {'stiffness': [B, 6, 6]}`` as the reference.  Per forward:
+
+1. the batch's receiver-sorted CSR is built once on the device (or taken from
+   ``batch.csr`` when the collate already made it) and every edge tensor is
+   permuted once into that order;
+2. ``eelg_edge_embed`` computes edge vectors, the 2x6 Gaussian edge features
+   and the l<=lmax spherical harmonics in one kernel;
+3. each ``MACELayer`` runs the fused HIP interaction and the HIP symmetric
+   contraction; channel-mixing linears and the readout tail are GEMMs;
+4. the per-graph mean pool is ``eelg_segment_sum_csr`` over the sorted
+   ``batch`` vector.
+"""
+from __future__ import annotations
+
+from argparse import Namespace
+from typing import Any, Dict
+
+import torch
+
+from . import ops
+from .blocks import (Cart_4_to_Mandel, GeneralNonLinearReadoutBlock, MACELayer, PositiveLayer,
+                     Spherical_to_Cartesian, as_csr)
+from .irreps import Irreps
+from .o3 import Linear
+
+
+class GNN_Head(torch.nn.Module):  # noqa: N801
+    def __init__(self, params: Namespace) -> None:
+        super().__init__()
+        self.params = params
+        hidden = Irreps(params.hidden_irreps)
+        self.number_of_edge_basis = params.num_edge_bases
+        node_ft_irreps = Irreps([(hidden.count("0e"), "0e")])
+        edge_feats_irreps = Irreps(f"{self.number_of_edge_basis * 2}x0e")
+        edge_attr_irreps = Irreps.spherical_harmonics(params.lmax)
+        num_features = hidden.count("0e")
+        interaction_irreps = (edge_attr_irreps * num_features).sort()[0].simplify()
+        readout_irreps = Irreps(params.readout_irreps)
+        self.num_interactions = params.message_passes
+
+        def layer(inp):
+            return MACELayer(inp, edge_attr_irreps, edge_feats_irreps, interaction_irreps, hidden,
+                             params.agg_norm_const, params.interaction_reduction, True,
+                             params.correlation, MLP_dim=params.inter_MLP_dim,
+                             MLP_layers=params.inter_MLP_layers)
+
+        self.layers = torch.nn.ModuleList([layer(node_ft_irreps)])
+        for _ in range(self.num_interactions - 1):
+            self.layers.append(layer(hidden))
+        self.nonlin_readout = GeneralNonLinearReadoutBlock(hidden, hidden, readout_irreps)
+        self.global_reduction = params.global_reduction
+        self.linear = Linear(readout_irreps, Irreps("2x0e+2x2e+1x4e"), biases=True)
+        self.sph_to_cart = Spherical_to_Cartesian()
+        self.cart_to_Mandel = Cart_4_to_Mandel()
+        self.positive_layer = PositiveLayer(params)
+
+    def forward(self, edge_index, node_ft, edge_sh, edge_feats, batch_idx, num_graphs: int):
+        csr, edge_sh, edge_feats = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_feats)
+        node_ft = self.layers[0](node_ft, csr, edge_sh, edge_feats)
+        for i in range(1, self.num_interactions):
+            node_ft = node_ft + self.layers[i](node_ft, csr, edge_sh, edge_feats)
+        out = self.nonlin_readout(node_ft)
+        graph_ft = ops.graph_pool(out, batch_idx, num_graphs, self.global_reduction)
+        stiff = self.sph_to_cart(self.linear(graph_ft))
+        return self.positive_layer(self.cart_to_Mandel(stiff))
+
+
+class EnergyEquivGNN(torch.nn.Module):
+    def __init__(self, params: Namespace, *args: Any, **kwargs: Any) -> None:
+        super().__init__(*args, **kwargs)
+        self.params = params
+        hidden = Irreps(params.hidden_irreps)
+        self.node_ft_embedding = torch.nn.Linear(1, hidden.count("0e"))
+        self.number_of_edge_basis = params.num_edge_bases
+        self.max_edge_radius = params.max_edge_radius
+        self.lmax = params.lmax
+        self.stiffness_head = GNN_Head(params)
+
+    @staticmethod
+    def edge_graph(batch) -> ops.EdgeCSR:
+        """Receiver-sorted CSR of ``batch.edge_index`` on its device (cached on the batch)."""
+        n = batch.node_attrs.shape[0]
+        dev = batch.edge_index.device
+        cached = getattr(batch, "_eelg_csr", None)
+        if cached is not None and cached.sender.device == dev and cached.num_nodes == n:
+            return cached
+        pre = getattr(batch, "csr", None)
+        if isinstance(pre, dict) and torch.is_tensor(pre.get("perm")):
+            csr = ops.EdgeCSR.from_dict({k: (v.to(dev) if torch.is_tensor(v) else v)
+                                         for k, v in pre.items()}, n)
+        else:
+            csr = ops.EdgeCSR.build(batch.edge_index, n)
+        try:
+            batch._eelg_csr = csr
+        except AttributeError:
+            pass
+        return csr
+
+    def forward(self, batch) -> Dict[str, torch.Tensor]:
+        csr = self.edge_graph(batch)
+        node_ft = self.node_ft_embedding(batch.node_attrs)
+        shifts = batch.shifts[csr.perm]
+        radius = batch.edge_attr[csr.perm].reshape(-1)
+        edge_sh, edge_feats = ops.edge_embed(batch.positions, csr, shifts, radius, self.lmax,
+                                             self.number_of_edge_basis, 0.6, self.max_edge_radius)
+        c = self.stiffness_head(csr, node_ft, edge_sh, edge_feats, batch.batch, batch.num_graphs)
+        return {"stiffness": c}

@@ -1,0 +1,214 @@
+"""PyTorch autograd wrappers over the C ABI (``include/eelg.h``).
+
+Every op requires HIP device tensors and launches on the current stream.
+There is no eager/CPU fallback: a missing library or a CPU tensor raises.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("the EnergyEquivGNN hot path runs only on a HIP device "
+                               "(got a CPU tensor); move the model and batch to 'cuda'")
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+def _i32(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.int32).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# edge graph in receiver-sorted order
+# ---------------------------------------------------------------------------
+@dataclass
+class EdgeCSR:
+    """Edges in receiver-sorted order.
+
+    ``perm`` maps the sorted order back to the caller's edge order
+    (``sorted_edge_j = original_edge[perm[j]]``).  ``rowptr`` is the receiver
+    CSR; ``sperm`` / ``srowptr`` group the sorted edges by sender."""
+    perm: torch.Tensor
+    sender: torch.Tensor
+    receiver: torch.Tensor
+    rowptr: torch.Tensor
+    sperm: torch.Tensor
+    srowptr: torch.Tensor
+    num_nodes: int
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.sender.shape[0])
+
+    @staticmethod
+    def from_dict(d: Dict, num_nodes: int) -> "EdgeCSR":
+        return EdgeCSR(d["perm"], d["sender"], d["receiver"], d["rowptr"], d["sperm"],
+                       d["srowptr"], num_nodes)
+
+    @staticmethod
+    def build(edge_index: torch.Tensor, num_nodes: int) -> "EdgeCSR":
+        from .data import build_edge_csr
+        return EdgeCSR.from_dict(build_edge_csr(edge_index, num_nodes), num_nodes)
+
+
+# ---------------------------------------------------------------------------
+# edge embedding (no gradient: positions and radii are data)
+# ---------------------------------------------------------------------------
+def edge_embed(pos, csr: EdgeCSR, shifts_sorted, radius_sorted, lmax: int, nb: int,
+               len_end: float, rad_end: float):
+    _require_device(pos, shifts_sorted, radius_sorted)
+    if pos.requires_grad or shifts_sorted.requires_grad:
+        raise NotImplementedError("gradients w.r.t. positions are not part of the hot path "
+                                  "(the reference never differentiates through geometry)")
+    e = csr.num_edges
+    sh = torch.empty(e, (lmax + 1) ** 2, device=pos.device, dtype=torch.float32)
+    feats = torch.empty(e, 2 * nb, device=pos.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.eelg_edge_embed(
+        _lib.ptr(_f32(pos)), _lib.ptr(csr.sender), _lib.ptr(csr.receiver),
+        _lib.ptr(_f32(shifts_sorted)), _lib.ptr(_f32(radius_sorted)), e, lmax, nb,
+        float(len_end), float(rad_end), _lib.ptr(sh), _lib.ptr(feats), _lib.stream()), "edge_embed")
+    return sh, feats
+
+
+# ---------------------------------------------------------------------------
+# CSR segmented sum
+# ---------------------------------------------------------------------------
+def segment_sum_csr(src, rowptr, n_rows: int, idx=None, row_scale=None, scale: float = 1.0):
+    _require_device(src)
+    src = _f32(src)
+    width = src[0].numel() if src.shape[0] > 0 else int(torch.tensor(src.shape[1:]).prod())
+    out = torch.empty((n_rows,) + tuple(src.shape[1:]), device=src.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.eelg_segment_sum_csr(
+        _lib.ptr(src), _lib.ptr(rowptr), _lib.ptr(idx), _lib.ptr(row_scale), float(scale), n_rows,
+        int(width), _lib.ptr(out), _lib.stream()), "segment_sum_csr")
+    return out
+
+
+class _SegmentMean(torch.autograd.Function):
+    """Per-graph mean/sum pool over sorted ``batch`` (``gnn/model.py:100-106``)."""
+
+    @staticmethod
+    def forward(ctx, src, ptr32, batch, inv_cnt):
+        ctx.save_for_backward(batch, inv_cnt)
+        return segment_sum_csr(src, ptr32, ptr32.shape[0] - 1, row_scale=inv_cnt)
+
+    @staticmethod
+    def backward(ctx, g):
+        batch, inv_cnt = ctx.saved_tensors
+        return (g * inv_cnt[:, None])[batch], None, None, None
+
+
+def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
+    _require_device(src)
+    cnt = torch.bincount(batch, minlength=num_graphs)
+    ptr = torch.zeros(num_graphs + 1, dtype=torch.int32, device=src.device)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    if reduce == "mean":
+        inv = 1.0 / cnt.clamp_min(1).to(torch.float32)
+    elif reduce == "sum":
+        inv = torch.ones(num_graphs, device=src.device, dtype=torch.float32)
+    else:
+        raise ValueError(f"global_reduction {reduce!r} not supported")
+    return _SegmentMean.apply(src, ptr, batch, inv)
+
+
+# ---------------------------------------------------------------------------
+# fused interaction: gather -> uvu tensor product -> segmented sum / norm
+# ---------------------------------------------------------------------------
+class _TPInteraction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
+        x, sh, w = _f32(x), _f32(sh), _f32(w)
+        n = x.shape[0]
+        if x.shape[1] != info["din"] or sh.shape[1] != info["nsh"] or w.shape[1] != info["wn"]:
+            raise ValueError(f"shape mismatch: x {tuple(x.shape)} sh {tuple(sh.shape)} "
+                             f"w {tuple(w.shape)} vs config {info}")
+        if sh.shape[0] != csr.num_edges or w.shape[0] != csr.num_edges or n != csr.num_nodes:
+            raise ValueError("edge/node counts do not match the CSR")
+        agg = torch.empty(n, info["dmid"], device=x.device, dtype=torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.eelg_tp_fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
+                                   _lib.ptr(csr.sender), _lib.ptr(csr.rowptr), n, float(inv_norm),
+                                   _lib.ptr(agg), _lib.stream()), "tp_fwd")
+        ctx.save_for_backward(x, sh, w)
+        ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm = csr, cfg, info, inv_norm
+        return agg
+
+    @staticmethod
+    def backward(ctx, g):
+        x, sh, w = ctx.saved_tensors
+        csr, info = ctx.csr, ctx.info
+        g = _f32(g)
+        e = csr.num_edges
+        gw = torch.empty_like(w)
+        gxe = torch.empty(e, info["din"], device=x.device, dtype=torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.eelg_tp_bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
+                                   _lib.ptr(csr.sender), _lib.ptr(csr.receiver), e, _lib.ptr(g),
+                                   float(ctx.inv_norm), _lib.ptr(gw), _lib.ptr(gxe), _lib.stream()),
+                   "tp_bwd")
+        gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
+        return gx, None, gw, None, None, None, None
+
+
+def tp_interaction(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
+    _require_device(x, sh, w)
+    return _TPInteraction.apply(x, sh, w, csr, cfg, info, inv_norm)
+
+
+# ---------------------------------------------------------------------------
+# symmetric contraction
+# ---------------------------------------------------------------------------
+class _SymCon(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int):
+        x, coef = _f32(x), _f32(coef)
+        n = x.shape[0]
+        if x.shape[1] != info["x_row"] or coef.shape != (mul, info["nterms"]):
+            raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
+        out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),
+                                   _lib.stream()), "sc_fwd")
+        ctx.save_for_backward(x, coef)
+        ctx.cfg, ctx.info, ctx.mul = cfg, info, mul
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, coef = ctx.saved_tensors
+        g = _f32(g)
+        n = x.shape[0]
+        lib = _lib.load()
+        gx = gcoef = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            _lib.check(lib.eelg_sc_bwd_x(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
+                                         ctx.mul, _lib.ptr(gx), _lib.stream()), "sc_bwd_x")
+        if ctx.needs_input_grad[1]:
+            chunk = max(64, min(4096, ((n + 15) // 16 + 63) // 64 * 64))
+            nch = (n + chunk - 1) // chunk
+            part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
+            _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(x), _lib.ptr(g), n, ctx.mul, chunk,
+                                            _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
+            gcoef = part.sum(0)
+        return gx, gcoef, None, None, None
+
+
+def symmetric_contraction(x, coef, cfg: int, info: Dict[str, int], mul: int):
+    _require_device(x, coef)
+    return _SymCon.apply(x, coef, cfg, info, mul)

@@ -1,0 +1,85 @@
+/*
+ * eelg.h -- C ABI of the MI355X-native EnergyEquivGNN message-passing hot path.
+ *
+ * Every entry point takes plain device pointers (fp32 data, int32 indices),
+ * sizes and a HIP stream (hipStream_t passed as void*), launches asynchronously
+ * on that stream and returns 0 on success or a negative code; the message of
+ * the last failure on the calling thread is in eelg_last_error().  Nothing here
+ * allocates, frees or synchronises, so every call can be captured in a hipGraph.
+ *
+ * Layout conventions (reference: gnn/datasets.py:256-269, e3nn mul-major rows):
+ *   node features   [N, sum_l mul*(2l+1)]   block (mul, l) laid out [mul][2l+1]
+ *   edge SH         [E, (lmax+1)^2]
+ *   TP weights      [E, npaths*mul]          index = path*mul + channel
+ *   edges           receiver-sorted; rowptr[N+1] is the receiver CSR,
+ *                   sperm/srowptr the sender CSR over the same edge order.
+ *
+ * Which reference interface each entry point replaces is given per function.
+ */
+#ifndef EELG_H
+#define EELG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Library / error handling ------------------------------------------------ */
+const char* eelg_version(void);
+const char* eelg_last_error(void);
+
+/* Config discovery: the irreps-specialised kernels are looked up by name
+ * ("tpA_l4" = 32x0e node irreps, "tpB_l4" = 32x0e+..+32x4e, "sc_l4_c3" ...).
+ * info receives {din, dmid, weight_numel, nsh, ngroups, npaths, lmax};
+ * sig is a structural hash the host re-derives to detect a stale build. */
+int eelg_tp_find(const char* name);
+int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
+/* info receives {D, x_row, out_row, nterms, n_term_groups} */
+int eelg_sc_find(const char* name);
+int eelg_sc_info(int cfg, int* info5, uint64_t* sig);
+
+/* Edge geometry + embeddings.
+ * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
+ * soft_one_hot_linspace x2 + cat (gnn/model.py:146-156) and
+ * o3.SphericalHarmonics(lmax, normalize=True, 'component') (gnn/model.py:126-129,157).
+ * feats[E, 2*nb] = [gauss(len; 0..len_end) | gauss(radius; 0..rad_end)]. */
+int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, const float* shifts,
+                    const float* radius, int n_edges, int lmax, int nb, float len_end,
+                    float rad_end, float* sh, float* feats, void* stream);
+
+/* Fused interaction: agg[n] = inv_norm * sum_{e: recv(e)=n} TP_uvu(x[sender(e)], sh[e], w[e]).
+ * Replaces conv_tp(node_feats[sender], edge_attrs, tp_weights) followed by
+ * scatter(..., reduce='sum') / agg_norm_const (gnn/blocks.py:591-597). */
+int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream);
+
+/* Backward of eelg_tp_fwd: grad_w[E, weight_numel] and per-edge grad of
+ * x[sender] gxe[E, din] (to be summed per sender with eelg_segment_sum_csr). */
+int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                float* grad_w, float* gxe, void* stream);
+
+/* CSR segmented sum (deterministic, no atomics):
+ * out[r, :] = scale * row_scale[r] * sum_{j in [rowptr[r], rowptr[r+1])} src[idx ? idx[j] : j, :].
+ * Replaces torch_scatter.scatter(..., reduce='sum'|'mean') (gnn/blocks.py:595-597,
+ * gnn/model.py:100-106) on sorted segments; row_scale may be NULL. */
+int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
+                         const float* row_scale, float scale, int n_rows, int width, float* out,
+                         void* stream);
+
+/* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
+ * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
+ * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms]. */
+int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
+                void* stream);
+int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
+                  int mul, float* grad_x, void* stream);
+/* partial[n_chunks, mul, nterms] with n_chunks = ceil(n_nodes / chunk); sum over chunks. */
+int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes, int mul,
+                     int chunk, float* partial, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EELG_H */
