@@ -47,8 +47,8 @@ def test_edge_embed_matches_oracle():
     er = oo3.soft_one_hot_linspace(b.edge_attr.double().squeeze(-1), 0, rmax, 6)
     ref_f = torch.cat([el, er], 1)
     p = perm.cpu()
-    assert rel_err(sh, ref_sh[p]) < 2e-6
-    assert rel_err(feats, ref_f[p]) < 2e-6
+    assert rel_err(sh, ref_sh[p]) < 1e-5      # fp32 recursion up to l=4
+    assert rel_err(feats, ref_f[p]) < 1e-5
 
 
 @pytest.mark.parametrize("width", [32, 800, 7360, 3])
