@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: lattice-graphs/s (fwd+bwd) of the 4-layer EnergyEquivGNN training step.
+
+Workload (BASELINE.json configs[1]; configs[2] at 8 GPUs): synthetic periodic
+lattices of 1024 nodes / 4096 directed edges, 32 graphs per GPU per step,
+4 message passes, the reference's network params (``scripts/train_main.py:25-52``).
+One step = forward + relative-MSE loss + backward + flat fp32 gradient
+all-reduce (N>1, RCCL) + grad-norm clip 10 + AdamW(amsgrad) step.  Graphs are
+sharded by graph id across ranks (weak scaling); inputs are resident in HBM
+before the timed region.
+
+Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 the driver
+uses ``torch.distributed.run`` and each rank reads RANK/LOCAL_RANK/WORLD_SIZE.
+Rank 0 prints one JSON line (roofline of the fused interaction kernel measured
+with HIP events over the timed region; CPU baseline = the oracle restatement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "energy-equiv-lattice-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def make_params(layers: int, max_edge_radius: float, lmax: int = 4):
+    from argparse import Namespace
+    hid = "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+    ro = "+".join(f"16x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+    return Namespace(lmax=lmax, hidden_irreps=hid, readout_irreps=ro, num_edge_bases=6,
+                     interaction_reduction="sum", interaction_bias=True, agg_norm_const=4.0,
+                     inter_MLP_dim=64, inter_MLP_layers=3, correlation=3, global_reduction="mean",
+                     message_passes=layers, positive_function="matrix_power_2",
+                     max_edge_radius=max_edge_radius, lr=1e-3, beta1=0.9, epsilon=1e-8,
+                     amsgrad=True, weight_decay=1e-8)
+
+
+def tp_fwd_bytes(n: int, e: int, din: int, w: int, dmid: int, nsh: int = 25) -> int:
+    """Algorithmic bytes of one fused-interaction launch ('Fused TP+scatter'):
+    x[N,Din] + sh[E,25] + w[E,W] + sender[E] + rowptr[N+1] (read) + agg[N,Dmid] (write)."""
+    return 4 * (n * din + e * nsh + e * w + e + (n + 1) + n * dmid)
+
+
+def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
+    """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
+    scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
+    shape: fwd + loss + bwd, median over steps within ``budget_s``."""
+    import oracle.model as om
+    from oracle.train import stiffness_loss
+    from gnn.data import collate
+    from gnn.synthetic import SyntheticLattices
+    ds = SyntheticLattices(1, n_nodes, n_edges, 1234)
+    b = collate([ds[0]])
+    torch.manual_seed(0)
+    m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius))
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        m.zero_grad(set_to_none=True)
+        loss = stiffness_loss(m(b)["stiffness"], b.stiffness)
+        loss.backward()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s or len(times) >= 10:
+            break
+    med = statistics.median(times)
+    return {"value": round(1.0 / med, 4), "unit": "lattice-graphs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} edges, "
+                      f"{layers} layers, median of {len(times)} step(s) ({med:.2f} s/step)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="graphs per GPU per step")
+    ap.add_argument("--nodes", type=int, default=1024)
+    ap.add_argument("--edges", type=int, default=4096)
+    ap.add_argument("--layers", type=int, default=4)
+    ap.add_argument("--lmax", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from gnn import EnergyEquivGNN, ops
+    from gnn.data import collate
+    from gnn.synthetic import SyntheticLattices
+    from gnn.train import stiffness_loss
+
+    # graphs rank*B .. rank*B+B-1 (graph-sharded, seed 1234 + global graph id)
+    ds = SyntheticLattices(args.batch * world, args.nodes, args.edges, 1234)
+    mine = [ds[rank * args.batch + g] for g in range(args.batch)]
+    rmax = torch.tensor([max(float(d.edge_attr.max()) for d in mine)], device=dev)
+    if world > 1:
+        dist.all_reduce(rmax, op=dist.ReduceOp.MAX)
+    params = make_params(args.layers, float(rmax.item()), args.lmax)
+    torch.manual_seed(0)
+    model = EnergyEquivGNN(params).to(dev)
+    opt = torch.optim.AdamW(model.parameters(), lr=params.lr, betas=(params.beta1, 0.999),
+                            eps=params.epsilon, amsgrad=params.amsgrad, weight_decay=params.weight_decay)
+    batch = collate(mine).to(dev)
+    model.edge_graph(batch)     # CSR built once per batch (collate-time work)
+    plist = [p for p in model.parameters()]
+    flat = torch.zeros(sum(p.numel() for p in plist), device=dev)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = stiffness_loss(model(batch)["stiffness"], batch.stiffness)
+        loss.backward()
+        if world > 1:
+            off = 0
+            for p in plist:
+                flat[off: off + p.numel()].copy_(p.grad.reshape(-1))
+                off += p.numel()
+            dist.all_reduce(flat)
+            flat.div_(world)
+            off = 0
+            for p in plist:
+                p.grad.copy_(flat[off: off + p.numel()].view_as(p))
+                off += p.numel()
+        torch.nn.utils.clip_grad_norm_(plist, 10.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.TIMER.enabled = True
+    ops.TIMER.records.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ksum = ops.TIMER.summary()
+
+    if rank == 0:
+        n_tot = args.batch * args.nodes
+        e_tot = args.batch * args.edges
+        key = "tp_fwd[din=800]" if args.lmax == 4 else "tp_fwd[din=512]"
+        lay = model.stiffness_head.layers[1].interaction
+        info = lay._config()[1]
+        roof = None
+        if key in ksum:
+            byts = tp_fwd_bytes(n_tot, e_tot, info["din"], info["wn"], info["dmid"], info["nsh"])
+            ms = ksum[key]["mean_ms"]
+            ach = byts / (ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": f"tp_fwd_tpB_l{args.lmax} (fused gather+TP+segmented sum)",
+                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum[key]["count"]}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget)
+        value = world * args.batch * args.steps / dt
+        out = {
+            "metric": "lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "lattice-graphs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic periodic lattices (SURVEY 8d generator), random-init weights",
+            "config": {"workload": f"EnergyEquivGNN {args.layers}-layer lmax{args.lmax}, "
+                                   f"{args.batch} graphs/GPU x {args.nodes} nodes/{args.edges} edges, "
+                                   "fwd+loss+bwd+allreduce+clip+AdamW",
+                       "global_batch": args.batch * world, "nodes_per_graph": args.nodes,
+                       "edges_per_graph": args.edges, "layers": args.layers,
+                       "parallelism": f"graph-sharded dp{world}"},
+            "loss": round(float(loss.item()), 6),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if args.kernel_summary:
+            print(json.dumps(ksum, indent=1), file=sys.stderr)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,6 +12,7 @@
 #include "../../include/eelg.h"
 #include "eelg_internal.h"
 #include "generated/eelg_gen.hip"
+#include "eelg_linear.hip"
 
 #define EELG_VERSION "eelg 0.1.0 gfx950"
 
@@ -238,6 +239,40 @@ int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes
   hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul / 4, c->njg), dim3(256), 0, (hipStream_t)stream, x,
                      grad_out, n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
+}
+
+int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
+                    float* y, int y_row, const eelg_lin_desc* desc, void* stream) {
+  if (!desc || desc->n_slots <= 0 || desc->n_slots > EELG_LIN_MAXSLOT)
+    return fail(-2, "linear_fwd: bad descriptor");
+  for (int s = 0; s < desc->n_slots; ++s) {
+    const eelg_lin_slot& sl = desc->slot[s];
+    if (sl.n_src < 0 || sl.n_src > EELG_LIN_MAXSRC || sl.d <= 0)
+      return fail(-2, "linear_fwd: bad slot %d", s);
+    for (int t = 0; t < sl.n_src; ++t)
+      if (sl.src[t].k <= 0) return fail(-2, "linear_fwd: empty K in slot %d", s);
+    if (sl.bias_off >= 0 && sl.d != 1) return fail(-2, "linear_fwd: bias on a non-scalar slot");
+  }
+  if (n_nodes <= 0) return 0;
+  dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, desc->max_jt);
+  hipLaunchKernelGGL(lin_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, w, bias,
+                     n_nodes, y, y_row, *desc);
+  return check_launch("linear_fwd");
+}
+
+int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,
+                      int rows_per_wave, float* partial, int n_partial, int w_total,
+                      const eelg_linw_desc* desc, void* stream) {
+  if (!desc || desc->n_ins <= 0 || desc->n_ins > EELG_LINW_MAXINS || rows_per_wave <= 0)
+    return fail(-2, "linear_bwd_w: bad descriptor");
+  const int slices = (desc->max_rows + rows_per_wave - 1) / rows_per_wave;
+  const int gx = (slices + 3) / 4;
+  if (n_partial < gx * 4) return fail(-2, "linear_bwd_w: partial has %d rows, need %d", n_partial, gx * 4);
+  if (n_nodes <= 0) return 0;
+  dim3 grid(gx, desc->n_ins, desc->max_ut * desc->max_jt);
+  hipLaunchKernelGGL(lin_bwdw_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g, g_row,
+                     n_nodes, rows_per_wave, partial, w_total, *desc);
+  return check_launch("linear_bwd_w");
 }
 
 }  // extern "C"

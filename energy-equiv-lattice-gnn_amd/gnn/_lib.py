@@ -32,7 +32,35 @@ _SIGS = {
     "eelg_sc_fwd": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
+    "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),
+    "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
 }
+
+LIN_MAXSRC, LIN_MAXSLOT, LINW_MAXINS = 4, 8, 8
+
+
+class LinSrc(ctypes.Structure):
+    _fields_ = [("x_off", _I), ("k", _I), ("w_off", _I), ("ldk", _I), ("ldj", _I), ("alpha", _F)]
+
+
+class LinSlot(ctypes.Structure):
+    _fields_ = [("y_off", _I), ("n_out", _I), ("d", _I), ("bias_off", _I), ("n_src", _I),
+                ("src", LinSrc * LIN_MAXSRC)]
+
+
+class LinDesc(ctypes.Structure):
+    _fields_ = [("n_slots", _I), ("max_jt", _I), ("max_rows", _I), ("pad", _I),
+                ("slot", LinSlot * LIN_MAXSLOT)]
+
+
+class LinWIns(ctypes.Structure):
+    _fields_ = [("x_off", _I), ("k", _I), ("g_off", _I), ("n_out", _I), ("d", _I), ("w_off", _I),
+                ("alpha", _F)]
+
+
+class LinWDesc(ctypes.Structure):
+    _fields_ = [("n_ins", _I), ("max_jt", _I), ("max_ut", _I), ("max_rows", _I),
+                ("ins", LinWIns * LINW_MAXINS)]
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

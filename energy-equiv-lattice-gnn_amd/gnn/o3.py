@@ -10,6 +10,7 @@
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from collections import Counter
 from typing import List, Tuple
@@ -20,7 +21,27 @@ from . import cg
 from .irreps import Irreps
 
 
+class _IrrepsLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, lin: "Linear"):
+        ctx.save_for_backward(x, weight)
+        ctx.lin = lin
+        return lin._fwd(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        lin = ctx.lin
+        gy = gy.contiguous()
+        gx = lin._bwd_x(gy, weight) if ctx.needs_input_grad[0] else None
+        gw = lin._bwd_w(x, gy) if ctx.needs_input_grad[1] else None
+        gb = lin._bwd_bias(gy) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None
+
+
 class Linear(torch.nn.Module):
+    """e3nn ``o3.Linear`` on mul-major rows; fp32-MFMA HIP kernels (``eelg_linear_*``)."""
+
     def __init__(self, irreps_in, irreps_out, internal_weights: bool = True,
                  shared_weights: bool = True, biases: bool = False):
         super().__init__()
@@ -43,29 +64,115 @@ class Linear(torch.nn.Module):
         else:
             self.register_parameter("bias", None)
         self._in_off, self._out_off = self.irreps_in.offsets(), self.irreps_out.offsets()
+        self._build_descriptors()
+
+    # -- descriptor tables for the C ABI (built once) ---------------------------
+    def _build_descriptors(self):
+        from . import _lib
+        w_offs, off = [], 0
+        for i, o in self.instructions:
+            w_offs.append(off)
+            off += self.irreps_in[i].mul * self.irreps_out[o].mul
+        self._w_offs = w_offs
+        b_offs, boff = {}, 0
+        for o in self.bias_slots:
+            b_offs[o] = boff
+            boff += self.irreps_out[o].mul
+        self._b_offs = b_offs
+
+        def slots(n_slots, dims, muls, offs, srcs, bias):
+            if n_slots > _lib.LIN_MAXSLOT:
+                raise NotImplementedError("too many irreps slots for eelg_linear")
+            desc = _lib.LinDesc()
+            desc.n_slots = n_slots
+            desc.max_jt = max((m + 31) // 32 for m in muls)
+            self_max_d = max(dims)
+            for s in range(n_slots):
+                sl = desc.slot[s]
+                sl.y_off, sl.n_out, sl.d = offs[s], muls[s], dims[s]
+                sl.bias_off = bias.get(s, -1)
+                if len(srcs[s]) > _lib.LIN_MAXSRC:
+                    raise NotImplementedError("too many sources for one irreps slot")
+                sl.n_src = len(srcs[s])
+                for t, (xo, k, wo, ldk, ldj, a) in enumerate(srcs[s]):
+                    sl.src[t].x_off, sl.src[t].k, sl.src[t].w_off = xo, k, wo
+                    sl.src[t].ldk, sl.src[t].ldj, sl.src[t].alpha = ldk, ldj, a
+            return desc, self_max_d
+
+        out_srcs = [[] for _ in self.irreps_out]
+        in_srcs = [[] for _ in self.irreps_in]
+        for (i, o), wo, a in zip(self.instructions, w_offs, self.alpha):
+            mi, mo = self.irreps_in[i].mul, self.irreps_out[o].mul
+            out_srcs[o].append((self._in_off[i], mi, wo, mo, 1, a))
+            in_srcs[i].append((self._out_off[o], mo, wo, 1, mo, a))
+        self._fwd_desc, self._fwd_maxd = slots(
+            len(self.irreps_out), [ir.dim for _, ir in self.irreps_out],
+            [m for m, _ in self.irreps_out], self._out_off, out_srcs, b_offs)
+        self._bx_desc, self._bx_maxd = slots(
+            len(self.irreps_in), [ir.dim for _, ir in self.irreps_in],
+            [m for m, _ in self.irreps_in], self._in_off, in_srcs, {})
+        if len(self.instructions) > _lib.LINW_MAXINS:
+            raise NotImplementedError("too many instructions for eelg_linear_bwd_w")
+        wd = _lib.LinWDesc()
+        wd.n_ins = len(self.instructions)
+        wd.max_jt = max([(self.irreps_out[o].mul + 31) // 32 for _, o in self.instructions] or [1])
+        wd.max_ut = max([(self.irreps_in[i].mul + 31) // 32 for i, _ in self.instructions] or [1])
+        for t, ((i, o), wo, a) in enumerate(zip(self.instructions, w_offs, self.alpha)):
+            e = wd.ins[t]
+            e.x_off, e.k, e.g_off = self._in_off[i], self.irreps_in[i].mul, self._out_off[o]
+            e.n_out, e.d, e.w_off, e.alpha = self.irreps_out[o].mul, self.irreps_in[i].ir.dim, wo, a
+        self._bw_desc = wd
+        self._bw_maxd = max([self.irreps_in[i].ir.dim for i, _ in self.instructions] or [1])
+
+    # -- launches ---------------------------------------------------------------
+    def _fwd(self, x, weight, bias):
+        from . import _lib
+        n = x.shape[0]
+        y = torch.empty(n, self.irreps_out.dim, device=x.device, dtype=torch.float32)
+        self._fwd_desc.max_rows = n * self._fwd_maxd
+        _lib.check(_lib.load().eelg_linear_fwd(
+            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(weight), _lib.ptr(bias), n, _lib.ptr(y),
+            self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream()), "linear_fwd")
+        return y
+
+    def _bwd_x(self, gy, weight):
+        from . import _lib
+        n = gy.shape[0]
+        gx = torch.empty(n, self.irreps_in.dim, device=gy.device, dtype=torch.float32)
+        self._bx_desc.max_rows = n * self._bx_maxd
+        _lib.check(_lib.load().eelg_linear_fwd(
+            _lib.ptr(gy), self.irreps_out.dim, _lib.ptr(weight), None, n, _lib.ptr(gx),
+            self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream()), "linear_bwd_x")
+        return gx
+
+    def _bwd_w(self, x, gy):
+        from . import _lib
+        n = x.shape[0]
+        if not self.instructions:
+            return torch.zeros_like(self.weight)
+        max_rows = n * self._bw_maxd
+        rpw = max(256, min(4096, (max_rows // 1024 + 1) // 2 * 2))
+        slices = (max_rows + rpw - 1) // rpw
+        n_part = (slices + 3) // 4 * 4
+        self._bw_desc.max_rows = max_rows
+        part = torch.empty(n_part, self.weight_numel, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().eelg_linear_bwd_w(
+            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, rpw,
+            _lib.ptr(part), n_part, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream()),
+            "linear_bwd_w")
+        return part.sum(0)
+
+    def _bwd_bias(self, gy):
+        parts = [gy[:, self._out_off[o]: self._out_off[o] + self.irreps_out[o].mul].sum(0)
+                 for o in self.bias_slots]
+        return torch.cat(parts)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        n = x.shape[0]
-        parts = [None] * len(self.irreps_out)
-        w_off = 0
-        for (i, o), a in zip(self.instructions, self.alpha):
-            mi, ir = self.irreps_in[i]
-            mo = self.irreps_out[o].mul
-            w = self.weight[w_off: w_off + mi * mo].view(mi, mo)
-            w_off += mi * mo
-            xi = x[:, self._in_off[i]: self._in_off[i] + mi * ir.dim].view(n, mi, ir.dim)
-            y = torch.matmul(xi.transpose(1, 2), w * a).transpose(1, 2)   # [n, mo, d]
-            parts[o] = y if parts[o] is None else parts[o] + y
-        out, b_off = [], 0
-        for o, (mo, ir) in enumerate(self.irreps_out):
-            y = parts[o]
-            if y is None:
-                y = x.new_zeros(n, mo, ir.dim)
-            if o in self.bias_slots:
-                y = y + self.bias[b_off: b_off + mo].view(1, mo, 1)
-                b_off += mo
-            out.append(y.reshape(n, mo * ir.dim))
-        return torch.cat(out, dim=1)
+        from .ops import _f32, _require_device
+        _require_device(x)
+        if x.shape[-1] != self.irreps_in.dim:
+            raise ValueError(f"Linear expects [..., {self.irreps_in.dim}], got {tuple(x.shape)}")
+        return _IrrepsLinearFn.apply(_f32(x), self.weight, self.bias, self)
 
 
 class Gate(torch.nn.Module):

@@ -13,6 +13,41 @@ import torch
 from . import _lib
 
 
+class KernelTimer:
+    """Optional HIP-event timing of selected launches (used by ``bench.py``).
+
+    Events are recorded on the current stream, the one every op launches on."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records: Dict[str, list] = {}
+
+    def start(self, name: str):
+        if not self.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return (name, ev)
+
+    def stop(self, tok) -> None:
+        if tok is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.setdefault(tok[0], []).append((tok[1], ev))
+
+    def summary(self) -> Dict[str, Dict[str, float]]:
+        torch.cuda.synchronize()
+        out = {}
+        for name, pairs in self.records.items():
+            ms = [a.elapsed_time(b) for a, b in pairs]
+            out[name] = {"count": len(ms), "mean_ms": sum(ms) / len(ms), "total_ms": sum(ms)}
+        return out
+
+
+TIMER = KernelTimer()
+
+
 def _require_device(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -141,9 +176,11 @@ class _TPInteraction(torch.autograd.Function):
             raise ValueError("edge/node counts do not match the CSR")
         agg = torch.empty(n, info["dmid"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
+        tok = TIMER.start(f"tp_fwd[din={info['din']}]")
         _lib.check(lib.eelg_tp_fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
                                    _lib.ptr(csr.sender), _lib.ptr(csr.rowptr), n, float(inv_norm),
                                    _lib.ptr(agg), _lib.stream()), "tp_fwd")
+        TIMER.stop(tok)
         ctx.save_for_backward(x, sh, w)
         ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm = csr, cfg, info, inv_norm
         return agg
@@ -157,10 +194,12 @@ class _TPInteraction(torch.autograd.Function):
         gw = torch.empty_like(w)
         gxe = torch.empty(e, info["din"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
+        tok = TIMER.start(f"tp_bwd[din={info['din']}]")
         _lib.check(lib.eelg_tp_bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
                                    _lib.ptr(csr.sender), _lib.ptr(csr.receiver), e, _lib.ptr(g),
                                    float(ctx.inv_norm), _lib.ptr(gw), _lib.ptr(gxe), _lib.stream()),
                    "tp_bwd")
+        TIMER.stop(tok)
         gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
         return gx, None, gw, None, None, None, None
 
@@ -182,8 +221,10 @@ class _SymCon(torch.autograd.Function):
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
         out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
+        tok = TIMER.start("sc_fwd")
         _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),
                                    _lib.stream()), "sc_fwd")
+        TIMER.stop(tok)
         ctx.save_for_backward(x, coef)
         ctx.cfg, ctx.info, ctx.mul = cfg, info, mul
         return out
@@ -197,14 +238,18 @@ class _SymCon(torch.autograd.Function):
         gx = gcoef = None
         if ctx.needs_input_grad[0]:
             gx = torch.empty_like(x)
+            tok = TIMER.start("sc_bwd_x")
             _lib.check(lib.eelg_sc_bwd_x(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
                                          ctx.mul, _lib.ptr(gx), _lib.stream()), "sc_bwd_x")
+            TIMER.stop(tok)
         if ctx.needs_input_grad[1]:
             chunk = max(64, min(4096, ((n + 15) // 16 + 63) // 64 * 64))
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
+            tok = TIMER.start("sc_bwd_coef")
             _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(x), _lib.ptr(g), n, ctx.mul, chunk,
                                             _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
+            TIMER.stop(tok)
             gcoef = part.sum(0)
         return gx, gcoef, None, None, None
 

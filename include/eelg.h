@@ -79,6 +79,28 @@ int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_
 int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes, int mul,
                      int chunk, float* partial, void* stream);
 
+/* Channel-mixing linear on mul-major irreps rows (o3.Linear, gnn/blocks.py:516-521,
+ * 553-559,471-476; gnn/model.py:82-86), fp32 MFMA.  A descriptor lists output
+ * slots; each slot sums alpha * x_block @ W over its sources, W element
+ * B[k][j] = w[w_off + k*ldk + j*ldj] (ldk = n_out, ldj = 1 forward; swapped for
+ * grad-x), plus bias[bias_off + j] on scalar slots (bias_off < 0: none). */
+#define EELG_LIN_MAXSRC 4
+#define EELG_LIN_MAXSLOT 8
+typedef struct { int x_off, k, w_off, ldk, ldj; float alpha; } eelg_lin_src;
+typedef struct { int y_off, n_out, d, bias_off, n_src; eelg_lin_src src[EELG_LIN_MAXSRC]; } eelg_lin_slot;
+typedef struct { int n_slots, max_jt, max_rows, pad; eelg_lin_slot slot[EELG_LIN_MAXSLOT]; } eelg_lin_desc;
+int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
+                    float* y, int y_row, const eelg_lin_desc* desc, void* stream);
+
+/* grad of the weights: partial[p, w_off + u*n_out + j] over row slices p (sum over p
+ * on the caller side; deterministic).  n_partial must be >= 4*ceil(max_slices/4). */
+#define EELG_LINW_MAXINS 8
+typedef struct { int x_off, k, g_off, n_out, d, w_off; float alpha; } eelg_linw_ins;
+typedef struct { int n_ins, max_jt, max_ut, max_rows; eelg_linw_ins ins[EELG_LINW_MAXINS]; } eelg_linw_desc;
+int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,
+                      int rows_per_wave, float* partial, int n_partial, int w_total,
+                      const eelg_linw_desc* desc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

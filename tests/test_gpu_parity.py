@@ -204,3 +204,35 @@ def test_model_batching_and_permutation_invariance():
         c0 = m(collate([d]).to(DEV))["stiffness"]
         c1 = m(collate([d2]).to(DEV))["stiffness"]
         assert rel_err(c1, c0) < 1e-5
+
+
+@pytest.mark.parametrize("irreps_in,irreps_out,bias,n", [
+    ("32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+32x1o+32x2e+32x3o+32x4e", False, 1000),
+    ("160x0e+256x1o+320x2e+320x3o+288x4e", "32x0e+32x1o+32x2e+32x3o+32x4e", True, 333),
+    ("32x0e+32x1o+32x2e+32x3o+32x4e", "160x0e+32x1o+32x2e+32x3o+32x4e", False, 257),
+    ("16x0e+16x1o+16x2e+16x3o+16x4e", "2x0e+2x2e+1x4e", True, 5),
+    ("32x0e+16x0e+32x1o", "32x0e+32x1o+8x2e", True, 70),   # fan-in of 2 sources, empty slot
+])
+def test_irreps_linear_fwd_bwd(irreps_in, irreps_out, bias, n):
+    from gnn.o3 import Linear
+    torch.manual_seed(3)
+    o = oo3.Linear(irreps_in, irreps_out, biases=bias).double()
+    m = Linear(irreps_in, irreps_out, biases=bias).to(DEV)
+    with torch.no_grad():
+        if bias:
+            o.bias.normal_()
+        for k, p in m.named_parameters():
+            p.copy_(dict(o.named_parameters())[k].float())
+    x = torch.randn(n, o.irreps_in.dim, dtype=torch.float64)
+    xo = x.clone().requires_grad_(True)
+    yo = o(xo)
+    g = torch.randn_like(yo)
+    (yo * g).sum().backward()
+    xm = x.float().to(DEV).requires_grad_(True)
+    ym = m(xm)
+    (ym * g.float().to(DEV)).sum().backward()
+    assert rel_err(ym, yo) < 2e-6
+    assert rel_err(xm.grad, xo.grad) < 2e-6
+    assert rel_err(m.weight.grad, o.weight.grad) < 5e-6
+    if bias:
+        assert rel_err(m.bias.grad, o.bias.grad) < 5e-6
