@@ -214,7 +214,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3((n_nodes + 63) / 64, mul / 4), dim3(256), 0,
+  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -224,20 +224,29 @@ int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_x, dim3((n_nodes + 63) / 64, mul / 4), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x);
   return check_launch("sc_bwd_x");
 }
 
-int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes, int mul,
-                     int chunk, float* partial, void* stream) {
+int eelg_sc_cmajor(int cfg, const float* x, int n_nodes, int mul, float* xt, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
-  if (chunk <= 0) return fail(-2, "sc_bwd_coef: chunk must be > 0");
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->cmajor, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, x, n_nodes, xt);
+  return check_launch("sc_cmajor");
+}
+
+int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int mul, int chunk,
+                     float* partial, void* stream) {
+  const eelg_sc_cfg* c = sc_get(cfg, mul);
+  if (!c) return -1;
+  if (chunk <= 0 || chunk % 64) return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of 64");
   if (n_nodes <= 0) return 0;
   const int nch = (n_nodes + chunk - 1) / chunk;
-  hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul / 4, c->njg), dim3(256), 0, (hipStream_t)stream, x,
-                     grad_out, n_nodes, chunk, partial);
+  hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + 7) / 8, nch, mul), dim3(512), 0,
+                     (hipStream_t)stream, xt, gt, n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
 }
 

@@ -10,6 +10,7 @@ typedef void (*eelg_tp_bwd_fn)(const float*, const float*, const float*, const i
 typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdc_fn)(const float*, const float*, int, int, float*);
+typedef void (*eelg_sc_cmajor_fn)(const float*, int, float*);
 
 struct eelg_tp_cfg {
   const char* name;
@@ -26,6 +27,7 @@ struct eelg_sc_cfg {
   eelg_sc_fwd_fn fwd;
   eelg_sc_bwdx_fn bwd_x;
   eelg_sc_bwdc_fn bwd_coef;
+  eelg_sc_cmajor_fn cmajor;
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

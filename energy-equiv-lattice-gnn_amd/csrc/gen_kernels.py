@@ -286,38 +286,87 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
 # ---------------------------------------------------------------------------
 # symmetric contraction
 # ---------------------------------------------------------------------------
+def pin(vs: List[str], memory: bool = False) -> str:
+    """Empty asm that 'modifies' every listed register and clobbers memory: a hard
+    boundary for the scheduler, so each term group computes in place (without it
+    hipcc hoists thousands of monomials / scalar coefficient loads and spills)."""
+    out = []
+    for k in range(0, len(vs), 10):
+        ops = ", ".join(f'"+v"({v})' for v in vs[k: k + 10])
+        out.append(f'asm volatile("" : {ops}{" : : " + chr(34) + "memory" + chr(34) if memory else ""});')
+    return " ".join(out)
+
+
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
+    """Symmetric contraction kernels.
+
+    Layout: x / out rows are e3nn mul-major ([l-block][channel][m]); a workgroup
+    of 4 waves owns 4 consecutive channels ("channel quad") x 64 nodes and stages
+    the quad's 4*D floats per node through LDS with contiguous global segments, so
+    every byte of x / out crosses HBM once.  One wave = one channel (wave-uniform,
+    coefficients come through scalar loads), one lane = one node."""
     plan = cg.symcon_plan(coupling, ls, corr)
     irs = [ir for _, ir in Irreps(coupling)]
+    assert tuple(ir.l for ir in irs) == tuple(ls), "in/out irreps must match"
     D = sum(ir.dim for ir in irs)
-    # per-component (l, m) of the 25-vector and its offset in the mul-major row
-    comp = []
-    off = 0
+    Q = 4                                   # channels per workgroup
+    QD = Q * D                              # floats per node in a quad tile
+    TP = QD + 1                             # padded LDS row (odd -> conflict-free)
+    comp = []                               # component a -> (l, m, row offset of block, seg start)
+    off = seg = 0
     for ir in irs:
         for m in range(ir.dim):
-            comp.append((ir.l, m, off))
+            comp.append((ir.l, m, off, seg))
         off += MUL * ir.dim
-    drow = off                                   # row width of x (= MUL * D)
-    ocomp = []
-    off = 0
-    for l in ls:
-        for m in range(2 * l + 1):
-            ocomp.append((l, m, off))
-        off += MUL * (2 * l + 1)
-    orow = off
+        seg += Q * ir.dim
+    drow = off
     nt = len(plan.terms)
 
-    def xaddr(a):
-        l, m, o = comp[a]
-        return f"{o} + c * {2 * l + 1} + {m}"
-
-    def oaddr(q):
-        l, m, o = ocomp[q]
-        return f"{o} + c * {2 * l + 1} + {m}"
+    def lq(a, cl):
+        """LDS column of component a for channel-in-quad cl (may be a runtime expr)."""
+        l, m, _, sg = comp[a]
+        return f"{sg} + ({cl}) * {2 * l + 1} + {m}"
 
     L: List[str] = []
     L.append(f"// ===== symmetric contraction config {name}: coupling {coupling}, correlation {corr} =====")
-    L.append(f"// {nt} polynomial terms per channel; x row {drow} floats, out row {orow} floats")
+    L.append(f"// {nt} polynomial terms per channel; rows of {drow} floats; quad tile {QD} floats/node")
+
+    # global offset of quad-tile column q for channel quad cq
+    L.append(f"__device__ __forceinline__ int sc_goff_{name}(int q, int cq) {{")
+    segs = []
+    o2 = s2 = 0
+    for ir in irs:
+        segs.append((s2, s2 + Q * ir.dim, o2, ir.dim))
+        o2 += MUL * ir.dim
+        s2 += Q * ir.dim
+    for (a, b, o, d) in segs[:-1]:
+        L.append(f"  if (q < {b}) return {o} + cq * {Q * d} + (q - {a});")
+    a, b, o, d = segs[-1]
+    L.append(f"  return {o} + cq * {Q * d} + (q - {a});")
+    L.append("}")
+
+    def stage_in(src, tile):
+        per = (64 * QD + 255) // 256
+        out = ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
+               "#pragma unroll 2",
+               f"  for (int it = 0; it < {per}; ++it) {{",
+               f"    const int idx = tid + 256 * it;",
+               f"    if (idx < {64 * QD}) {{",
+               f"      const int nl = idx / {QD}, q = idx - nl * {QD}, n = n0 + nl;",
+               f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {drow} + sc_goff_{name}(q, cq)] : 0.0f;",
+               "    }", "  } }"]
+        return out
+
+    def stage_out(dst, tile):
+        per = (64 * QD + 255) // 256
+        return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
+                "#pragma unroll 2",
+                f"  for (int it = 0; it < {per}; ++it) {{",
+                f"    const int idx = tid + 256 * it;",
+                f"    if (idx < {64 * QD}) {{",
+                f"      const int nl = idx / {QD}, q = idx - nl * {QD}, n = n0 + nl;",
+                f"      if (n < n_nodes) {dst}[(size_t)n * {drow} + sc_goff_{name}(q, cq)] = {tile}[nl * {TP} + q];",
+                "    }", "  } }"]
 
     # group terms by (a, b) pair
     pairs: Dict[Tuple[int, int], Dict] = {}
@@ -332,19 +381,26 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             else:
                 g["d3"].setdefault(c, []).append((t, q))
 
+    head = ["  const int cq = blockIdx.x;", "  const int n0 = blockIdx.y * 64;",
+            "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
+            f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + wv);",
+            f"  const int cl = __builtin_amdgcn_readfirstlane(wv);",
+            f"  const float* __restrict__ cf = coef + (size_t)c * {nt};"]
+
     # ---------------- forward ----------------
     L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
-    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));")
-    L.append("  const int n = blockIdx.x * 64 + (threadIdx.x & 63);")
-    L.append(f"  const float* __restrict__ cf = coef + (size_t)c * {nt};")
-    L.append("  if (n >= n_nodes) return;")
-    L.append(f"  const float* __restrict__ xr = x + (size_t)n * {drow};")
+    L.append(f"  __shared__ float tile[64 * {TP}];")
+    L += head
+    L += stage_in("x", "tile")
+    L.append("  __syncthreads();")
+    L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
     for a in range(D):
-        L.append(f"  const float x{a} = xr[{xaddr(a)}];")
-    for q in range(len(ocomp)):
+        L.append(f"  float x{a} = tr[{lq(a, 'cl')}];")
+    for q in range(D):
         L.append(f"  float o{q} = 0.0f;")
+    fpin = pin([f"x{a}" for a in range(D)] + [f"o{q}" for q in range(D)])
     for t, a, q in deg1:
         L.append(f"  o{q} = fmaf(cf[{t}], x{a}, o{q});")
     for (a, b), g in pairs.items():
@@ -357,26 +413,32 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 L.append(f"      o{q} = fmaf(cf[{t}], m, o{q});")
             L.append("    }")
         L.append("  }")
-    L.append(f"  float* __restrict__ orow = out + (size_t)n * {orow};")
-    for q in range(len(ocomp)):
-        L.append(f"  orow[{oaddr(q)}] = o{q};")
+        L.append("  " + fpin)
+    L.append("  __syncthreads();")
+    for q in range(D):
+        L.append(f"  tr[{lq(q, 'cl')}] = o{q};")
+    L.append("  __syncthreads();")
+    L += stage_out("out", "tile")
     L.append("}")
 
     # ---------------- backward w.r.t. x ----------------
     L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx) {")
-    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));")
-    L.append("  const int n = blockIdx.x * 64 + (threadIdx.x & 63);")
-    L.append(f"  const float* __restrict__ cf = coef + (size_t)c * {nt};")
-    L.append("  if (n >= n_nodes) return;")
-    L.append(f"  const float* __restrict__ xr = x + (size_t)n * {drow};")
-    L.append(f"  const float* __restrict__ gr = gout + (size_t)n * {orow};")
+    L.append(f"  __shared__ float tx[64 * {TP}];")
+    L.append(f"  __shared__ float tg[64 * {TP}];")
+    L += head
+    L += stage_in("x", "tx")
+    L += stage_in("gout", "tg")
+    L.append("  __syncthreads();")
+    L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
+    L.append(f"  const float* __restrict__ gr = tg + lane * {TP};")
     for a in range(D):
-        L.append(f"  const float x{a} = xr[{xaddr(a)}];")
+        L.append(f"  float x{a} = xr[{lq(a, 'cl')}];")
         L.append(f"  float d{a} = 0.0f;")
-    for q in range(len(ocomp)):
-        L.append(f"  const float g{q} = gr[{oaddr(q)}];")
+    for q in range(D):
+        L.append(f"  float g{q} = gr[{lq(q, 'cl')}];")
+    bpin = pin([f"x{a}" for a in range(D)] + [f"g{q}" for q in range(D)] + [f"d{a}" for a in range(D)])
     for t, a, q in deg1:
         L.append(f"  d{a} = fmaf(cf[{t}], g{q}, d{a});")
     for (a, b), g in pairs.items():
@@ -389,30 +451,76 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 L.append(f"      s = fmaf(cf[{t}], g{q}, s);")
             L.append(f"      d{cc} = fmaf(s, p, d{cc}); s2 = fmaf(s, x{cc}, s2); }}")
         L.append(f"    d{a} = fmaf(s2, x{b}, d{a}); d{b} = fmaf(s2, x{a}, d{b}); }}")
-    L.append(f"  float* __restrict__ gxr = gx + (size_t)n * {drow};")
+        L.append("  " + bpin)
+    L.append("  __syncthreads();")
     for a in range(D):
-        L.append(f"  gxr[{xaddr(a)}] = d{a};")
+        L.append(f"  xr[{lq(a, 'cl')}] = d{a};")
+    L.append("  __syncthreads();")
+    L += stage_out("gx", "tx")
+    L.append("}")
+
+    # ---------------- mul-major -> channel-major transpose ----------------
+    # dst[(c * D + a) * n_nodes + n] = src[n, a-th component of channel c]
+    L.append(f"__global__ __launch_bounds__(256) void sc_cmajor_{name}(")
+    L.append("    const float* __restrict__ x, int n_nodes, float* __restrict__ xt) {")
+    L.append(f"  __shared__ float tile[64 * {TP}];")
+    L.append("  const int cq = blockIdx.x;")
+    L.append("  const int n0 = blockIdx.y * 64;")
+    L += stage_in("x", "tile")
+    L.append("  __syncthreads();")
+    sgs = ", ".join(str(comp[a][3]) for a in range(D))
+    dls = ", ".join(str(2 * comp[a][0] + 1) for a in range(D))
+    ms = ", ".join(str(comp[a][1]) for a in range(D))
+    L.append(f"  const int kseg[{D}] = {{{sgs}}}, kd[{D}] = {{{dls}}}, km[{D}] = {{{ms}}};")
+    per = (Q * D * 64 + 255) // 256
+    L.append(f"  for (int it = 0; it < {per}; ++it) {{")
+    L.append("    const int idx = threadIdx.x + 256 * it;")
+    L.append(f"    if (idx < {Q * D * 64}) {{")
+    L.append("      const int row = idx >> 6, nl = idx & 63, n = n0 + nl;")
+    L.append(f"      const int cl = row / {D}, a = row - cl * {D};")
+    L.append(f"      if (n < n_nodes) xt[(size_t)((cq * {Q} + cl) * {D} + a) * n_nodes + n] = "
+             f"tile[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];")
+    L.append("    }")
+    L.append("  }")
     L.append("}")
 
     # ---------------- backward w.r.t. coefficients ----------------
-    JG = 128
+    JG = 64
+    WPB = 8
     groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
-    L.append(f"// coefficient gradient: {len(groups)} term groups of <= {JG}; each wave = 1 channel x 64 lanes,")
-    L.append("// lanes walk the nodes of one chunk and keep per-term partial sums in registers,")
-    L.append("// reduced over lanes through an LDS transpose at the end.")
-    L.append(f"__global__ __launch_bounds__(256) void sc_bwd_coef_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ gout, int n_nodes, int chunk,")
+    L.append(f"// coefficient gradient from channel-major x / g: {len(groups)} term groups of <= {JG};")
+    L.append(f"// a workgroup = one channel x {WPB} term groups (waves) sharing staged 64-node tiles;")
+    L.append("// per-lane partial sums over the chunk, then a recursive-halving lane reduction.")
+    L.append(f"__global__ __launch_bounds__({64 * WPB}) void sc_bwd_coef_{name}(")
+    L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
-    L.append("  __shared__ float red[4][64 * 33];")
+    L.append(f"  __shared__ float sx[{D} * 64];")
+    L.append(f"  __shared__ float sg[{D} * 64];")
+    L.append("  const int c = blockIdx.z;")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
-    L.append("  const int c = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + wv);")
-    L.append("  const int n0 = blockIdx.x * chunk;")
-    L.append("  const int n1 = min(n_nodes, n0 + chunk);")
-    L.append(f"  float* __restrict__ dst = part + ((size_t)blockIdx.x * {MUL} + c) * {nt};")
-    L.append("  float* __restrict__ r = red[wv];")
-    L.append("  switch (blockIdx.z) {")
+    L.append(f"  const int jg = __builtin_amdgcn_readfirstlane(blockIdx.x * {WPB} + wv);")
+    L.append(f"  const float* __restrict__ xs = xt + (size_t)c * {D} * n_nodes;")
+    L.append(f"  const float* __restrict__ gs = gt + (size_t)c * {D} * n_nodes;")
+    L.append("  const int nb = blockIdx.y * chunk;")
+    L.append("  const int ne = min(n_nodes, nb + chunk);")
+    L.append(f"  float acc[{JG}];")
+    L.append("#pragma unroll")
+    L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = 0.0f;")
+    L.append("  for (int n0 = nb; n0 < ne; n0 += 64) {")
+    per = (D * 64 + 64 * WPB - 1) // (64 * WPB)
+    L.append(f"    for (int it = 0; it < {per}; ++it) {{")
+    L.append(f"      const int idx = threadIdx.x + {64 * WPB} * it;")
+    L.append(f"      if (idx < {D * 64}) {{")
+    L.append("        const int a = idx >> 6, n = n0 + (idx & 63);")
+    L.append("        const bool ok = n < ne;")
+    L.append("        sx[idx] = ok ? xs[(size_t)a * n_nodes + n] : 0.0f;")
+    L.append("        sg[idx] = ok ? gs[(size_t)a * n_nodes + n] : 0.0f;")
+    L.append("      }")
+    L.append("    }")
+    L.append("    __syncthreads();")
+    L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
-        L.append(f"  case {gi}: {{")
+        L.append(f"    case {gi}: {{")
         need_x, need_g = set(), set()
         for t in grp:
             nu, (a, b, cc), q = plan.terms[t]
@@ -422,50 +530,57 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 need_x.add(b)
             if nu >= 3:
                 need_x.add(cc)
-        for t in grp:
-            L.append(f"    float s{t} = 0.0f;")
-        L.append("    for (int n = n0 + lane; n < n1; n += 64) {")
-        L.append(f"      const float* __restrict__ xr = x + (size_t)n * {drow};")
-        L.append(f"      const float* __restrict__ gr = gout + (size_t)n * {orow};")
         for a in sorted(need_x):
-            L.append(f"      const float x{a} = xr[{xaddr(a)}];")
+            L.append(f"      const float x{a} = sx[{a * 64} + lane];")
         for q in sorted(need_g):
-            L.append(f"      const float g{q} = gr[{oaddr(q)}];")
-        cur_pair = None
-        for t in grp:
+            L.append(f"      const float g{q} = sg[{q * 64} + lane];")
+        cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
+        cur = None
+        for jj, t in enumerate(grp):
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
-                L.append(f"      s{t} = fmaf(x{a}, g{q}, s{t});")
+                L.append(f"      acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
                 continue
-            if cur_pair != (a, b):
-                if cur_pair is not None:
+            if cur != (a, b):
+                if cur is not None:
                     L.append("      }")
+                    L.append("      " + cpin)
                 L.append(f"      {{ const float p = x{a} * x{b};")
-                cur_pair = (a, b)
+                cur = (a, b)
             if nu == 2:
-                L.append(f"        s{t} = fmaf(p, g{q}, s{t});")
+                L.append(f"        acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
             else:
-                L.append(f"        s{t} = fmaf(p * x{cc}, g{q}, s{t});")
-        if cur_pair is not None:
+                L.append(f"        acc[{jj}] = fmaf(p * x{cc}, g{q}, acc[{jj}]);")
+        if cur is not None:
             L.append("      }")
-        L.append("    }")
-        # transpose-reduce in chunks of 32 terms
-        for s0 in range(0, len(grp), 32):
-            sub = grp[s0: s0 + 32]
-            for jj, t in enumerate(sub):
-                L.append(f"    r[lane * 33 + {jj}] = s{t};")
-            L.append("    __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_wave_barrier();")
-            L.append("    { float acc = 0.0f; const int col = lane & 31, half = lane >> 5;")
-            L.append("      #pragma unroll")
-            L.append("      for (int rr = 0; rr < 32; ++rr) acc += r[(half * 32 + rr) * 33 + col];")
-            L.append("      acc += __shfl_xor(acc, 32);")
-            L.append(f"      if (lane < {len(sub)}) dst[{grp[s0]} + lane] = acc; }}")
-            L.append("    __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_wave_barrier();")
-        L.append("    break; }")
-    L.append("  default: break;")
+        L.append("      break; }")
+    L.append("    default: break;")
+    L.append("    }")
+    L.append("    __syncthreads();")
+    L.append("  }")
+    # recursive-halving reduction over the 6 lane bits: with R = JG / 64 values left
+    # per lane, lane L ends with terms R*L + i (i < R)
+    assert JG % 64 == 0
+    n = JG
+    for bit in (32, 16, 8, 4, 2, 1):
+        h = n // 2
+        L.append(f"  {{ const bool up = (lane & {bit}) != 0;")
+        for i in range(h):
+            L.append(f"    {{ const float keep = up ? acc[{i + h}] : acc[{i}]; "
+                     f"const float give = up ? acc[{i}] : acc[{i + h}]; "
+                     f"acc[{i}] = keep + __shfl_xor(give, {bit}); }}")
+            if i % 8 == 7:
+                L.append("    " + pin([f"acc[{t}]" for t in range(i - 7, i + 1)], memory=False))
+        L.append("  }")
+        n = h
+    R = JG // 64
+    L.append(f"  if (jg < {len(groups)}) {{")
+    L.append(f"    float* __restrict__ dst = part + ((size_t)blockIdx.y * {MUL} + c) * {nt};")
+    for i in range(R):
+        L.append(f"    {{ const int t = jg * {JG} + {R} * lane + {i}; if (t < {nt}) dst[t] = acc[{i}]; }}")
     L.append("  }")
     L.append("}")
-    info = dict(D=D, drow=drow, orow=orow, nterms=nt, njg=len(groups),
+    info = dict(D=D, drow=drow, orow=drow, nterms=nt, njg=len(groups), wpb=WPB,
                 sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -497,7 +612,7 @@ def main(outdir: str) -> None:
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, '
-                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}}},')
+                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

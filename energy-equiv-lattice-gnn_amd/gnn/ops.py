@@ -243,11 +243,19 @@ class _SymCon(torch.autograd.Function):
                                          ctx.mul, _lib.ptr(gx), _lib.stream()), "sc_bwd_x")
             TIMER.stop(tok)
         if ctx.needs_input_grad[1]:
-            chunk = max(64, min(4096, ((n + 15) // 16 + 63) // 64 * 64))
+            xt = torch.empty(ctx.mul * ctx.info["D"], n, device=x.device, dtype=torch.float32)
+            gt = torch.empty_like(xt)
+            tok = TIMER.start("sc_cmajor")
+            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
+                                          _lib.stream()), "sc_cmajor")
+            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
+                                          _lib.stream()), "sc_cmajor")
+            TIMER.stop(tok)
+            chunk = max(64, min(4096, (n // 16 + 63) // 64 * 64))
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
             tok = TIMER.start("sc_bwd_coef")
-            _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(x), _lib.ptr(g), n, ctx.mul, chunk,
+            _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul, chunk,
                                             _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
             TIMER.stop(tok)
             gcoef = part.sum(0)

@@ -75,8 +75,12 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
                   int mul, float* grad_x, void* stream);
-/* partial[n_chunks, mul, nterms] with n_chunks = ceil(n_nodes / chunk); sum over chunks. */
-int eelg_sc_bwd_coef(int cfg, const float* x, const float* grad_out, int n_nodes, int mul,
+/* Channel-major copy xt[(c*D + a)*N + n] of a mul-major row tensor (feeds sc_bwd_coef). */
+int eelg_sc_cmajor(int cfg, const float* x, int n_nodes, int mul, float* xt, void* stream);
+/* Coefficient gradient from channel-major x and grad_out:
+ * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk) (chunk % 64 == 0);
+ * the caller sums over chunks (deterministic). */
+int eelg_sc_bwd_coef(int cfg, const float* xt, const float* grad_out_t, int n_nodes, int mul,
                      int chunk, float* partial, void* stream);
 
 /* Channel-mixing linear on mul-major irreps rows (o3.Linear, gnn/blocks.py:516-521,
