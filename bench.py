@@ -121,24 +121,16 @@ def main():
                             eps=params.epsilon, amsgrad=params.amsgrad, weight_decay=params.weight_decay)
     batch = collate(mine).to(dev)
     model.edge_graph(batch)     # CSR built once per batch (collate-time work)
+    from gnn.parallel import FlatGradAllReduce, broadcast_parameters
+    broadcast_parameters(model)
     plist = [p for p in model.parameters()]
-    flat = torch.zeros(sum(p.numel() for p in plist), device=dev)
+    allreduce = FlatGradAllReduce(plist)
 
     def step():
         opt.zero_grad(set_to_none=False)
         loss = stiffness_loss(model(batch)["stiffness"], batch.stiffness)
         loss.backward()
-        if world > 1:
-            off = 0
-            for p in plist:
-                flat[off: off + p.numel()].copy_(p.grad.reshape(-1))
-                off += p.numel()
-            dist.all_reduce(flat)
-            flat.div_(world)
-            off = 0
-            for p in plist:
-                p.grad.copy_(flat[off: off + p.numel()].view_as(p))
-                off += p.numel()
+        allreduce()                      # one flat fp32 RCCL all-reduce (no-op at N=1)
         torch.nn.utils.clip_grad_norm_(plist, 10.0)
         opt.step()
         return loss

@@ -1,0 +1,174 @@
+"""Host-side logic (CPU): product constants vs the oracle, data path / CSR, the
+generator's structural plans, and the C-ABI library (loads, exports, config
+tables) -- no kernel launches."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import oracle.mace as omace
+import oracle.o3 as oo3
+from gnn import cg
+from gnn.data import Batch, build_edge_csr, collate
+from gnn.irreps import Irreps
+from gnn.synthetic import SyntheticLattices, make_lattice
+
+
+def test_product_cg_matches_oracle():
+    for l1 in range(5):
+        for l2 in range(5):
+            for l3 in range(abs(l1 - l2), l1 + l2 + 1):
+                a = cg.wigner_3j(l1, l2, l3)
+                b = oo3.wigner_3j(l1, l2, l3).numpy()
+                assert np.abs(a - b).max() < 1e-12, (l1, l2, l3)
+
+
+def test_product_sh_matches_oracle():
+    v = np.random.default_rng(0).normal(size=(50, 3))
+    a = cg.spherical_harmonics_np(4, v)
+    b = oo3.spherical_harmonics(4, torch.tensor(v)).numpy()
+    assert np.abs(a - b).max() < 1e-12
+
+
+def test_product_u_matrices_match_oracle():
+    for l in range(5):
+        ir = oo3.Irreps(str(oo3.Irrep(l, (-1) ** l)))
+        for nu in (1, 2, 3):
+            a = cg.U_matrix("0e+1o+2e+3o+4e", l, nu)
+            b = omace.U_matrix_real(oo3.Irreps("0e+1o+2e+3o+4e"), ir, nu)[-1].numpy()
+            assert np.abs(a.reshape(b.shape) - b).max() < 1e-12
+
+
+def test_product_change_of_basis_matches_oracle():
+    assert np.abs(cg.stiffness_change_of_basis() - oo3.stiffness_change_of_basis().numpy()).max() < 1e-12
+
+
+@pytest.mark.parametrize("lmax", [2, 3, 4])
+def test_symcon_polynomial_equals_dense_contraction(lmax):
+    """The sparse symmetrised polynomial behind the HIP kernels equals the reference's
+    dense U.W contraction (gnn/mace.py:242-277)."""
+    coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+    hid = "+".join(f"8x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+    plan = cg.symcon_plan(coupling, tuple(range(lmax + 1)), 3)
+    torch.manual_seed(0)
+    sc = omace.SymmetricContraction(oo3.Irreps(hid), oo3.Irreps(hid), 3).double()
+    ws = []
+    for l, nu, k in plan.weight_blocks:
+        w = sc.contractions[f"8x{oo3.Irrep(l, (-1) ** l)}"].weights[str(nu)]
+        assert w.shape == (k, 8)
+        ws.append(w.detach())
+    coef = plan.ubig @ torch.cat(ws).numpy()
+    D = plan.D
+    x = np.random.default_rng(1).normal(size=(4, 8, D))
+    out = np.zeros((4, 8, D))
+    for t, (nu, (a, b, c), o) in enumerate(plan.terms):
+        m = x[:, :, a] * (x[:, :, b] if nu >= 2 else 1) * (x[:, :, c] if nu >= 3 else 1)
+        out[:, :, o] += coef[t] * m
+    with torch.no_grad():
+        ref = sc(torch.tensor(x)).numpy()
+    mine = np.concatenate([out[:, :, l * l:(l + 1) ** 2].reshape(4, -1) for l in range(lmax + 1)], 1)
+    assert np.abs(mine - ref).max() < 1e-6 * np.abs(ref).max()
+
+
+def test_irreps_sort_simplify_semantics():
+    ir = Irreps("1x2e+3x0e+2x1o+1x0e")
+    s, p = ir.sort()
+    assert str(s) == "3x0e+1x0e+2x1o+1x2e" and p == [3, 0, 2, 1]
+    assert str(s.simplify()) == "4x0e+2x1o+1x2e"
+    assert (Irreps.spherical_harmonics(4) * 32).sort()[0].simplify().dim == 800
+
+
+def test_synthetic_lattice_layout():
+    d = make_lattice(64, 256, 5)
+    ei = d.edge_index
+    e = ei.shape[1]
+    assert e == 256 and d.node_attrs.shape == (64, 1) and torch.all(d.node_attrs == 1)
+    h = e // 2
+    assert torch.equal(ei[:, :h], ei.flip(0)[:, h:])                 # reversed copies
+    assert torch.allclose(d.shifts[:h], -d.shifts[h:])
+    assert torch.equal(d.edge_attr[:h], d.edge_attr[h:])
+    vec = d.positions[ei[1]] - d.positions[ei[0]] + d.shifts
+    a = 0.54 * 64 ** (1 / 3)
+    assert float(vec.norm(dim=-1).max()) <= math.sqrt(3) * a / 2 + 1e-5  # minimum image
+    ev = torch.linalg.eigvalsh(d.stiffness[0].double())
+    assert (ev > 0).all()
+
+
+def test_collate_and_csr():
+    ds = SyntheticLattices(3, 20, 80, 3)
+    b = collate([ds[i] for i in range(3)])
+    assert b.num_graphs == 3 and b.stiffness.shape == (3, 6, 6)
+    assert torch.equal(b.batch, torch.repeat_interleave(torch.arange(3), 20))
+    assert int(b.edge_index[:, 80:160].min()) >= 20 and int(b.edge_index[:, 80:160].max()) < 40
+    assert torch.equal(b["stiffness"], b.stiffness)
+    csr = build_edge_csr(b.edge_index, 60)
+    recv = b.edge_index[1][csr["perm"]]
+    assert torch.all(recv[1:] >= recv[:-1])
+    cnt = torch.bincount(b.edge_index[1], minlength=60)
+    assert torch.equal(csr["rowptr"][1:].long() - csr["rowptr"][:-1].long(), cnt)
+    s = csr["sender"].long()[csr["sperm"].long()]
+    assert torch.all(s[1:] >= s[:-1])
+    assert torch.equal(torch.sort(csr["sperm"].long())[0], torch.arange(240))
+
+
+def test_csr_handles_isolated_nodes_and_empty_graph():
+    ei = torch.tensor([[0, 2], [2, 0]])
+    csr = build_edge_csr(ei, 4)
+    assert csr["rowptr"].tolist() == [0, 1, 1, 2, 2]
+    csr0 = build_edge_csr(torch.zeros(2, 0, dtype=torch.long), 3)
+    assert csr0["rowptr"].tolist() == [0, 0, 0, 0] and csr0["perm"].numel() == 0
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    import os
+    import re
+    from gnn import _lib
+    lib = _lib.load()
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "eelg.h")).read()
+    declared = set(re.findall(r"\b(eelg_[a-z0-9_]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.eelg_version().startswith(b"eelg")
+
+
+def test_library_config_tables_match_host_structure():
+    from gnn import _lib
+    for lmax in (3, 4):
+        sh = Irreps.spherical_harmonics(lmax)
+        target = (sh * 32).sort()[0].simplify()
+        hid = Irreps("+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+        for name, node in ((f"tpA_l{lmax}", Irreps("32x0e")), (f"tpB_l{lmax}", hid)):
+            _, info, sig = _lib.tp_config(name)
+            paths = cg.tp_paths(node, sh, target)
+            assert info["din"] == node.dim and info["npaths"] == len(paths)
+            assert info["wn"] == 32 * len(paths) and info["nsh"] == sh.dim
+            assert sig == cg.fnv1a64(cg.tp_signature(node, sh, target))
+        coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+        _, info, sig = _lib.sc_config(f"sc_l{lmax}_c3")
+        plan = cg.symcon_plan(coupling, tuple(range(lmax + 1)), 3)
+        assert info["nterms"] == len(plan.terms) and info["x_row"] == 32 * plan.D
+        assert sig == cg.fnv1a64(cg.sc_signature(coupling, tuple(range(lmax + 1)), 3))
+    with pytest.raises(_lib.EELGError):
+        _lib.tp_config("no_such_config")
+
+
+def test_product_rejects_cpu_tensors_loudly():
+    from gnn import ops
+    from gnn.o3 import Linear
+    lin = Linear("4x0e", "4x0e")
+    with pytest.raises(RuntimeError, match="HIP device"):
+        lin(torch.randn(3, 4))
+
+
+def test_product_model_param_names_match_oracle():
+    from helpers import params
+    from gnn.model import EnergyEquivGNN
+    import oracle.model as omodel
+    p = params(2)
+    m, o = EnergyEquivGNN(p), omodel.EnergyEquivGNN(p)
+    pm = {k: v.shape for k, v in m.named_parameters()}
+    po = {k: v.shape for k, v in o.named_parameters()}
+    assert pm == po
+    assert sum(v.numel() for v in m.parameters()) == 223186

@@ -24,7 +24,12 @@ from gnn.blocks import TensorProductInteractionBlock  # noqa: E402
 from gnn.irreps import Irreps  # noqa: E402
 
 
+ONLY = None
+
+
 def timeit(fn, reps):
+    if reps == 0:
+        return float("nan")
     for _ in range(3):
         fn()
     ts = []
@@ -42,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--graphs", type=int, default=32)
+    ap.add_argument("--only", default="", help="regex: time only matching ops")
     args = ap.parse_args()
     dev = "cuda"
     ds = SyntheticLattices(args.graphs, 1024, 4096, 1234)
@@ -53,7 +59,17 @@ def main():
     sh_ir = Irreps.spherical_harmonics(4)
     res = {}
 
+    import re as _re
+
+    def want(name):
+        return not args.only or _re.search(args.only, name)
+
+    def timeit_if(name, fn, reps):
+        return timeit(fn, reps) if want(name) else float("nan")
+
     def rec(name, ms, bytes_=None, flops=None):
+        if not want(name):
+            return
         r = {"ms": round(ms, 4)}
         if bytes_:
             r["GB/s"] = round(bytes_ / ms / 1e6, 1)
@@ -65,7 +81,7 @@ def main():
 
     sh, feats = ops.edge_embed(b.positions, csr, b.shifts[csr.perm], b.edge_attr[csr.perm].reshape(-1),
                                4, 6, 0.6, 0.05)
-    rec("edge_embed", timeit(lambda: ops.edge_embed(b.positions, csr, b.shifts[csr.perm],
+    rec("edge_embed", timeit_if("edge_embed", lambda: ops.edge_embed(b.positions, csr, b.shifts[csr.perm],
                                                      b.edge_attr[csr.perm].reshape(-1), 4, 6, 0.6, 0.05),
                              args.reps))
     blk = TensorProductInteractionBlock(hid, sh_ir, "12x0e", hid, 4.0).to(dev)
@@ -75,7 +91,7 @@ def main():
     agg = ops.tp_interaction(x, sh, w, csr, idx, info, 0.25)
     tp_bytes = 4 * (n * 800 + e * 25 + e * info["wn"] + e + n + 1 + n * info["dmid"])
     tp_flops = 2 * 32 * 1302 * e
-    rec("tp_fwd (B)", timeit(lambda: ops.tp_interaction(x, sh, w, csr, idx, info, 0.25), args.reps),
+    rec("tp_fwd (B)", timeit_if("tp_fwd (B)", lambda: ops.tp_interaction(x, sh, w, csr, idx, info, 0.25), args.reps),
         tp_bytes, tp_flops)
     g = torch.randn_like(agg)
     gw = torch.empty_like(w)
@@ -88,12 +104,11 @@ def main():
                                        ops._lib.ptr(g), 0.25, ops._lib.ptr(gw), ops._lib.ptr(gxe),
                                        ops._lib.stream()), "tp_bwd")
     bwd_bytes = 4 * (n * 800 + e * 25 + 2 * e * info["wn"] + 2 * e + e * 800 + n * info["dmid"])
-    rec("tp_bwd (B)", timeit(tpb, args.reps), bwd_bytes, 2 * tp_flops)
-    rec("segment_sum gxe->gx (800)",
-        timeit(lambda: ops.segment_sum_csr(gxe, csr.srowptr, n, idx=csr.sperm), args.reps),
+    rec("tp_bwd (B)", timeit_if("tp_bwd (B)", tpb, args.reps), bwd_bytes, 2 * tp_flops)
+    rec("segment_sum gxe->gx (800)", timeit_if("segment_sum gxe->gx (800)", lambda: ops.segment_sum_csr(gxe, csr.srowptr, n, idx=csr.sperm), args.reps),
         4 * (e * 800 + n * 800 + 2 * e))
     m7360 = torch.randn(e, 7360, device=dev)
-    rec("segment_sum unfused (7360)", timeit(lambda: ops.segment_sum_csr(m7360, csr.rowptr, n), args.reps),
+    rec("segment_sum unfused (7360)", timeit_if("segment_sum unfused (7360)", lambda: ops.segment_sum_csr(m7360, csr.rowptr, n), args.reps),
         4 * (e * 7360 + n * 7360 + e))
     del m7360
     sc = SymmetricContraction(hid, hid, 3).to(dev)
@@ -101,7 +116,7 @@ def main():
     coef = sc.coefficients().detach()
     xs = torch.randn(n, 800, device=dev)
     nt = sinfo["nterms"]
-    rec("sc_fwd", timeit(lambda: ops.symmetric_contraction(xs, coef, sidx, sinfo, 32), args.reps),
+    rec("sc_fwd", timeit_if("sc_fwd", lambda: ops.symmetric_contraction(xs, coef, sidx, sinfo, 32), args.reps),
         4 * 2 * n * 800, 2 * n * 32 * (nt + 3250))
     gs = torch.randn(n, 800, device=dev)
     gx = torch.empty_like(xs)
@@ -109,14 +124,14 @@ def main():
     def scbx():
         ops._lib.check(lib.eelg_sc_bwd_x(sidx, ops._lib.ptr(xs), ops._lib.ptr(coef), ops._lib.ptr(gs), n,
                                          32, ops._lib.ptr(gx), ops._lib.stream()), "bx")
-    rec("sc_bwd_x", timeit(scbx, args.reps), 4 * 3 * n * 800, 2 * n * 32 * (nt + 2 * 3250))
+    rec("sc_bwd_x", timeit_if("sc_bwd_x", scbx, args.reps), 4 * 3 * n * 800, 2 * n * 32 * (nt + 2 * 3250))
     xt = torch.empty(800, n, device=dev)
     gt = torch.empty(800, n, device=dev)
 
     def cm():
         ops._lib.check(lib.eelg_sc_cmajor(sidx, ops._lib.ptr(xs), n, 32, ops._lib.ptr(xt),
                                           ops._lib.stream()), "cm")
-    rec("sc_cmajor", timeit(cm, args.reps), 4 * 2 * n * 800)
+    rec("sc_cmajor", timeit_if("sc_cmajor", cm, args.reps), 4 * 2 * n * 800)
     cm()
     ops._lib.check(lib.eelg_sc_cmajor(sidx, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream()), "cm")
     chunk = max(64, min(4096, (n // 16 + 63) // 64 * 64))
@@ -126,7 +141,7 @@ def main():
     def scbc():
         ops._lib.check(lib.eelg_sc_bwd_coef(sidx, ops._lib.ptr(xt), ops._lib.ptr(gt), n, 32, chunk,
                                             ops._lib.ptr(part), ops._lib.stream()), "bc")
-    rec("sc_bwd_coef", timeit(scbc, args.reps), None, 2 * n * 32 * (nt + 3250))
+    rec("sc_bwd_coef", timeit_if("sc_bwd_coef", scbc, args.reps), None, 2 * n * 32 * (nt + 3250))
     for name, ii, oo in [("lin 800->800", hid, hid),
                          ("lin 7360->800", "160x0e+256x1o+320x2e+320x3o+288x4e", hid)]:
         lin = Linear(ii, oo).to(dev)
@@ -135,18 +150,18 @@ def main():
         byt = 4 * n * (lin.irreps_in.dim + lin.irreps_out.dim)
         fl = 2 * n * sum(lin.irreps_in[i].mul * lin.irreps_out[o].mul * lin.irreps_in[i].ir.dim
                          for i, o in lin.instructions)
-        rec(f"{name} fwd", timeit(lambda: lin._fwd(xi, lin.weight, None), args.reps), byt, fl)
-        rec(f"{name} bwd_x", timeit(lambda: lin._bwd_x(gy, lin.weight), args.reps), byt, fl)
-        rec(f"{name} bwd_w", timeit(lambda: lin._bwd_w(xi, gy), args.reps), byt, fl)
+        rec(f"{name} fwd", timeit_if(f"{name} fwd", lambda: lin._fwd(xi, lin.weight, None), args.reps), byt, fl)
+        rec(f"{name} bwd_x", timeit_if(f"{name} bwd_x", lambda: lin._bwd_x(gy, lin.weight), args.reps), byt, fl)
+        rec(f"{name} bwd_w", timeit_if(f"{name} bwd_w", lambda: lin._bwd_w(xi, gy), args.reps), byt, fl)
     mlp = blk.conv_tp_weights
     ef = torch.randn(e, 12, device=dev, requires_grad=True)
-    rec("radial MLP fwd (torch)", timeit(lambda: mlp(ef), args.reps), None,
+    rec("radial MLP fwd (torch)", timeit_if("radial MLP fwd (torch)", lambda: mlp(ef), args.reps), None,
         2 * e * (12 * 64 + 64 * 64 + 64 * info["wn"]))
 
     def mlpfb():
         out = mlp(ef)
         out.backward(torch.ones_like(out))
-    rec("radial MLP fwd+bwd (torch)", timeit(mlpfb, args.reps), None,
+    rec("radial MLP fwd+bwd (torch)", timeit_if("radial MLP fwd+bwd (torch)", mlpfb, args.reps), None,
         3 * 2 * e * (12 * 64 + 64 * 64 + 64 * info["wn"]))
     print(json.dumps(res))
 
