@@ -159,7 +159,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     wn = sum(p.mul for p in paths)
     for p in paths:
         assert p.mul == MUL
-    groups = _group_paths(paths, 48)
+    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), 32)
     node_ls = [ir.l for _, ir in node]
     node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
     L: List[str] = []
@@ -194,10 +194,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         for l in need_l1:
             d = 2 * l + 1
             for i in range(d):
-                L.append(f"      const float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
+                L.append(f"      float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
         for l in need_l2:
             for j in range(2 * l + 1):
-                L.append(f"      const float y{l * l + j} = ye[{l * l + j}];")
+                L.append(f"      float y{l * l + j} = ye[{l * l + j}];")
+        gpin = pin([f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+                   + [f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
+                   + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)])
         for p in grp:
             L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
             L.append(f"        const float wp = we[{p.slot * MUL}] * ({flit(p.coef)} * inv_norm);")
@@ -205,6 +208,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
             for k in range(2 * p.l3 + 1):
                 L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
             L.append("      }")
+            L.append("      " + gpin)
         L.append("    }")
         for p in grp:
             d3 = 2 * p.l3 + 1
@@ -241,11 +245,14 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         d = 2 * l + 1
         L.append(f"  case {gi}: {{ // input block l1 = {l}")
         for i in range(d):
-            L.append(f"    const float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
+            L.append(f"    float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
             L.append(f"    float gx{l}_{i} = 0.0f;")
-        for l2 in sorted({p.l2 for p in grp}):
+        l2s = sorted({p.l2 for p in grp})
+        for l2 in l2s:
             for j in range(2 * l2 + 1):
-                L.append(f"    const float y{l2 * l2 + j} = ye[{l2 * l2 + j}];")
+                L.append(f"    float y{l2 * l2 + j} = ye[{l2 * l2 + j}];")
+        bpin_ = pin([f"x{l}_{i}" for i in range(d)] + [f"gx{l}_{i}" for i in range(d)]
+                    + [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)])
         for p in grp:
             d3 = 2 * p.l3 + 1
             d1 = 2 * p.l1 + 1
@@ -271,6 +278,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                 if ts:
                     L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
             L.append("    }")
+            L.append("    " + bpin_)
         for i in range(d):
             L.append(f"    gxo[{node_off[l]} + u * {d} + {i}] = gx{l}_{i};")
         L.append("    break; }")
@@ -506,18 +514,27 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  float acc[{JG}];")
     L.append("#pragma unroll")
     L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = 0.0f;")
-    L.append("  for (int n0 = nb; n0 < ne; n0 += 64) {")
+    # double-buffered staging: the next tile's global loads are in flight (in
+    # registers) while the current tile is consumed from LDS
     per = (D * 64 + 64 * WPB - 1) // (64 * WPB)
-    L.append(f"    for (int it = 0; it < {per}; ++it) {{")
-    L.append(f"      const int idx = threadIdx.x + {64 * WPB} * it;")
-    L.append(f"      if (idx < {D * 64}) {{")
-    L.append("        const int a = idx >> 6, n = n0 + (idx & 63);")
-    L.append("        const bool ok = n < ne;")
-    L.append("        sx[idx] = ok ? xs[(size_t)a * n_nodes + n] : 0.0f;")
-    L.append("        sg[idx] = ok ? gs[(size_t)a * n_nodes + n] : 0.0f;")
-    L.append("      }")
-    L.append("    }")
+    for it in range(per):
+        L.append(f"  float rx{it} = 0.0f, rg{it} = 0.0f;")
+
+    def issue(base):
+        out = []
+        for it in range(per):
+            out.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; const int a = idx >> 6, n = {base} + (idx & 63);")
+            out.append(f"      if (idx < {D * 64} && n < ne) {{ rx{it} = xs[(size_t)a * n_nodes + n]; rg{it} = gs[(size_t)a * n_nodes + n]; }}"
+                       f" else {{ rx{it} = 0.0f; rg{it} = 0.0f; }} }}")
+        return out
+    L += issue("nb")
+    L.append("  for (int n0 = nb; n0 < ne; n0 += 64) {")
+    for it in range(per):
+        L.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) {{ sx[idx] = rx{it}; sg[idx] = rg{it}; }} }}")
     L.append("    __syncthreads();")
+    L.append("    if (n0 + 64 < ne) {")
+    L += issue("n0 + 64")
+    L.append("    }")
     L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
         L.append(f"    case {gi}: {{")
