@@ -51,6 +51,25 @@ def tp_fwd_bytes(n: int, e: int, din: int, w: int, dmid: int, nsh: int = 25) -> 
     return 4 * (n * din + e * nsh + e * w + e + (n + 1) + n * dmid)
 
 
+def pmc_traffic(kernel: str, args) -> dict | None:
+    """HBM bytes per launch of ``kernel`` from the committed PMC table (profiles/pmc_traffic.json,
+    written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
+    of this same default command).  Only valid for the default workload; None otherwise."""
+    if (args.batch, args.nodes, args.edges, args.layers, args.lmax) != (32, 1024, 4096, 4, 4):
+        return None
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    tab = json.load(open(path))
+    hits = [v for k, v in tab["kernels"].items() if k.split("|")[0] == kernel]
+    if not hits:
+        return None
+    t = max(hits, key=lambda v: sum(v.values()))
+    fetch, write = t.get("FETCH_SIZE", 0.0), t.get("WRITE_SIZE", 0.0)
+    return {"bytes": round(fetch + write), "fetch": round(fetch), "write": round(write),
+            "source": f"profiles/pmc_traffic.json ({tab['source']})"}
+
+
 def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
     """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
     scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
@@ -168,9 +187,12 @@ def main():
             ms = ksum[key]["mean_ms"]
             ach = byts / (ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBPS, 4),
+                    "traffic": None, "traffic_detail": pmc_traffic(f"tp_fwd_tpB_l{args.lmax}", args),
                     "kernel": f"tp_fwd_tpB_l{args.lmax} (fused gather+TP+segmented sum)",
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum[key]["count"]}
+            if roof["traffic_detail"]:
+                roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget)

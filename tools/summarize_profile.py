@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_round.sh output dir into the committed evidence under profiles/.
+
+  python tools/summarize_profile.py gpurun_out/r01a r01a
+
+writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_summary.md         top kernels per step + bench line + PMC traffic table
+  profiles/pmc_traffic.json         per-kernel mean FETCH_SIZE / WRITE_SIZE bytes per launch
+
+Counter units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  WRITE_SIZE is exact for
+our stores (tp_fwd writes N*7360*4 B and the counter reads exactly that); the gfx950 "FETCH
+halving" (MI355X_MICROARCH.md, HBM) applies to 16-B/lane streaming reads only -- our kernels
+read 4-B/lane rows, and the sc_cmajor transpose (reads x once, 104.9 MB) reports 1.2x its
+bytes, so FETCH_SIZE is used raw here (calibration recorded in the summary).
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, tag):
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    bench = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
+    b = json.loads(bench)
+    steps_traced = 7           # profile_round.sh: --steps 5 --warmup 2
+    lines = [f"# Profile {tag}", "",
+             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 "
+             "--no-cpu-baseline` (7 traced steps); bench line from `python3 bench.py --steps "
+             f"{b['steps']} --warmup {b['warmup']}` on the same box.", "",
+             f"bench: **{b['value']} {b['unit']}**, {b['ms_per_step']} ms/step; roofline kernel "
+             f"{b['roofline']['kernel']}: {b['roofline']['mean_ms']} ms/launch (HIP events), "
+             f"{b['roofline']['achieved']} GB/s = {b['roofline']['frac']*100:.1f}% of 8 TB/s", "",
+             f"kernel time traced: {tot/1e6:.1f} ms = {tot/1e6/steps_traced:.2f} ms/step", "",
+             "| % | calls/step | avg us | kernel |", "|---|---|---|---|"]
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
+        lines.append(f"| {float(r['TotalDurationNs'])/tot*100:.1f} | {int(r['Calls'])/steps_traced:.1f} | "
+                     f"{float(r['AverageNs'])/1e3:.1f} | `{r['Name'][:80]}` |")
+    traffic = collections.defaultdict(dict)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        d = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            d[(r["Kernel_Name"].split("(")[0], r["Grid_Size"])].append(float(r["Counter_Value"]) * 1024)
+        for (k, g), v in d.items():
+            traffic[f"{k}|{g}"][c] = sum(v) / len(v)
+    lines += ["", "## HBM traffic per launch (PMC, separate FETCH_SIZE / WRITE_SIZE passes, KiB x 1024)", "",
+              "| kernel | grid | FETCH MB | WRITE MB |", "|---|---|---|---|"]
+    for key in sorted(traffic, key=lambda k: -sum(traffic[k].values()))[:20]:
+        k, g = key.split("|")
+        t = traffic[key]
+        lines.append(f"| `{k[:60]}` | {g} | {t.get('FETCH_SIZE', 0)/1e6:.1f} | {t.get('WRITE_SIZE', 0)/1e6:.1f} |")
+    open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    json.dump({"source": tag, "unit": "bytes per launch", "kernels": traffic},
+              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+    print("\n".join(lines[:40]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
