@@ -263,24 +263,30 @@ int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias
     if (sl.bias_off >= 0 && sl.d != 1) return fail(-2, "linear_fwd: bias on a non-scalar slot");
   }
   if (n_nodes <= 0) return 0;
-  dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, desc->max_jt);
+  dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, 1);  // column tiles loop in-kernel
   hipLaunchKernelGGL(lin_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, w, bias,
                      n_nodes, y, y_row, *desc);
   return check_launch("linear_fwd");
 }
 
 int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,
-                      int rows_per_wave, float* partial, int n_partial, int w_total,
+                      int nodes_per_slice, float* partial, int n_partial, int w_total,
                       const eelg_linw_desc* desc, void* stream) {
-  if (!desc || desc->n_ins <= 0 || desc->n_ins > EELG_LINW_MAXINS || rows_per_wave <= 0)
+  if (!desc || desc->n_ins <= 0 || desc->n_ins > EELG_LINW_MAXINS || nodes_per_slice <= 0)
     return fail(-2, "linear_bwd_w: bad descriptor");
-  const int slices = (desc->max_rows + rows_per_wave - 1) / rows_per_wave;
-  const int gx = (slices + 3) / 4;
-  if (n_partial < gx * 4) return fail(-2, "linear_bwd_w: partial has %d rows, need %d", n_partial, gx * 4);
+  for (int t = 0; t < desc->n_ins; ++t) {
+    const eelg_linw_ins& in = desc->ins[t];
+    if (in.k <= 0 || in.n_out <= 0 || in.d <= 0 || in.d > 32)
+      return fail(-2, "linear_bwd_w: bad instruction %d", t);
+    if ((in.k + 31) / 32 > desc->max_ut || (in.n_out + 31) / 32 > desc->max_jt)
+      return fail(-2, "linear_bwd_w: max_ut/max_jt too small for instruction %d", t);
+  }
   if (n_nodes <= 0) return 0;
-  dim3 grid(gx, desc->n_ins, desc->max_ut * desc->max_jt);
+  const int slices = (n_nodes + nodes_per_slice - 1) / nodes_per_slice;
+  if (n_partial < slices) return fail(-2, "linear_bwd_w: partial has %d rows, need %d", n_partial, slices);
+  dim3 grid(slices, desc->n_ins, desc->max_ut * desc->max_jt);
   hipLaunchKernelGGL(lin_bwdw_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g, g_row,
-                     n_nodes, rows_per_wave, partial, w_total, *desc);
+                     n_nodes, nodes_per_slice, partial, w_total, *desc);
   return check_launch("linear_bwd_w");
 }
 

@@ -4,112 +4,310 @@
 // For one output slot (mul_out copies of an irrep of dimension d):
 //   y[n, j, m] = sum_src alpha_src * sum_u x[n, x_off + u*d + m] * W[u, j]   (+ bias[j] if d == 1)
 // i.e. a GEMM whose rows are (node, component) pairs, K = mul_in, N = mul_out.
-// One wave computes a 32-row x 32-column tile with v_mfma_f32_32x32x2_f32
-// (exact f32: a k-ordered fmaf chain).  The same kernel serves grad-x with
-// the transposed weight (ldk/ldj swapped).  grad-W reduces over rows with
-// deterministic per-wave partials (summed on the host side).
+//
+// HBM access is the cost (the 7360 -> 800 interaction linear moves ~1 GB per call at
+// 16 FLOP/B), so every global access is a contiguous per-node run: a node's block of one
+// irrep is K*d consecutive floats, and a 32-wide K chunk of it is 32*d consecutive floats.
+// A workgroup owns 128 consecutive (node, m) rows of one slot; it stages each K chunk of
+// those rows into LDS as A[row][k] with float4 loads, the matching 32x32 weight tile as
+// B[k][j], runs v_mfma_f32_32x32x2_f32 (one 32-row tile per wave; exact f32 products),
+// and writes the output tile back through LDS as per-node contiguous runs.  grad-x uses
+// the same kernel with the transposed weight (ldk/ldj swapped).  grad-W reduces over
+// rows into deterministic per-slice partials (summed on the host side).
 #include <hip/hip_runtime.h>
 
 typedef float eelg_f32x16 __attribute__((ext_vector_type(16)));
+
+#define LIN_ROWS 128           // rows per workgroup (4 waves x 32)
+#define LIN_KC 32              // K chunk
+#define LIN_ST 33              // LDS row stride in floats (conflict-free column reads)
+
+// Walks a flat index f = a * (W*d) + b*d + m in steps of `step` without divisions in the
+// loop (a = node in the run list, b = channel in [0, W), m = component in [0, d)).
+struct Walk3 {
+  int a, b, m;
+  int da, db, dm;
+  __device__ void init(int f, int step, int W, int d) {
+    const int seg = W * d;
+    a = f / seg;
+    const int r = f - a * seg;
+    b = r / d;
+    m = r - b * d;
+    da = step / seg;
+    const int rr = step - da * seg;
+    db = rr / d;
+    dm = rr - db * d;
+  }
+  __device__ void next(int W, int d) {
+    a += da;
+    b += db;
+    m += dm;
+    if (m >= d) { m -= d; ++b; }
+    if (b >= W) { b -= W; ++a; }
+  }
+};
+
+// Register-staged copy of one A chunk (<= LIN_NV float4 per thread) and one B tile.
+#define LIN_NV 5
+
+struct ChunkRef {
+  int x_off, k, kc, w_off, ldk, ldj;
+  float alpha;
+};
+
+__device__ __forceinline__ ChunkRef lin_chunk(const eelg_lin_slot& sl, int c) {
+  int s = 0, base = 0;
+  for (;;) {
+    const int nc = (sl.src[s].k + LIN_KC - 1) / LIN_KC;
+    if (c < base + nc || s + 1 >= sl.n_src) break;
+    base += nc;
+    ++s;
+  }
+  const eelg_lin_src& src = sl.src[s];
+  ChunkRef r;
+  r.x_off = src.x_off;
+  r.k = src.k;
+  r.kc = (c - base) * LIN_KC;
+  r.w_off = src.w_off;
+  r.ldk = src.ldk;
+  r.ldj = src.ldj;
+  r.alpha = src.alpha;
+  return r;
+}
 
 __global__ __launch_bounds__(256) void lin_fwd_kernel(const float* __restrict__ x, int x_row,
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ bias, int n_nodes,
                                                       float* __restrict__ y, int y_row,
                                                       eelg_lin_desc desc) {
+  __shared__ float As[LIN_ROWS * LIN_ST];
+  __shared__ float Bs[LIN_KC * LIN_ST];
+  __shared__ float Os[LIN_ROWS * LIN_ST];
   const eelg_lin_slot& sl = desc.slot[blockIdx.y];
   const int d = sl.d;
   const int rows = n_nodes * d;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile0 = (blockIdx.x * 4 + wave) * 32;
-  const int jt = blockIdx.z * 32;
-  if (tile0 >= rows || jt >= sl.n_out) return;
-  const int kh = lane >> 5;
-  const int r = tile0 + (lane & 31);
-  const bool rok = r < rows;
-  const int n = rok ? r / d : 0;
-  const int m = rok ? r - n * d : 0;
-  const int j = jt + (lane & 31);
-  const bool jok = j < sl.n_out;
-  eelg_f32x16 acc;
+  const int r0 = blockIdx.x * LIN_ROWS;
+  if (r0 >= rows) return;  // uniform per workgroup
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n_lo = r0 / d;
+  const int n_hi = min(n_nodes, (r0 + LIN_ROWS + d - 1) / d);  // exclusive
+  const int span = n_hi - n_lo;
+  const int seg = LIN_KC * d;
+  const int total = span * seg;  // flat (node, k, m) entries of one chunk
+  int n_chunks = 0;
+  for (int s = 0; s < sl.n_src; ++s) n_chunks += (sl.src[s].k + LIN_KC - 1) / LIN_KC;
+  const int n_jt = (sl.n_out + 31) / 32;
+  // float4 staging needs 16-B aligned per-node runs and <= LIN_NV float4 per thread
+  bool vec = (x_row & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && total <= LIN_NV * 1024;
+  for (int s = 0; s < sl.n_src; ++s) vec = vec && (sl.src[s].x_off & 3) == 0 && (sl.src[s].k & 3) == 0;
+
+  float4 va[LIN_NV];
+  float vb[4];
+  // issue the global loads of chunk c (A rows into va, B tile into vb)
+  auto load_chunk = [&](int c, int jt, bool with_a) {
+    const ChunkRef ch = lin_chunk(sl, c);
+    const int kk = min(LIN_KC, ch.k - ch.kc);
+    if (vec && with_a) {
+      const float* __restrict__ xb = x + (size_t)n_lo * x_row + ch.x_off + (size_t)ch.kc * d;
+      const int len = kk * d;
+      Walk3 cw;
+      cw.init(4 * tid, 4 * 256, LIN_KC, d);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-  for (int s = 0; s < sl.n_src; ++s) {
-    const eelg_lin_src& src = sl.src[s];
-    const float* __restrict__ xa = x + (size_t)n * x_row + src.x_off + m + kh * d;
-    const float* __restrict__ wb = w + src.w_off + (size_t)j * src.ldj + kh * src.ldk;
-    const float al = src.alpha;
-    const int xs = 2 * d, ws = 2 * src.ldk;
-    const int k_even = src.k & ~1;
-#pragma unroll 8
-    for (int kk = 0; kk < k_even; kk += 2) {
-      const float a = rok ? xa[(kk >> 1) * xs] : 0.0f;
-      const float b = jok ? wb[(kk >> 1) * ws] * al : 0.0f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      for (int q = 0; q < LIN_NV; ++q) {
+        const int f = 4 * tid + 1024 * q;
+        const int within = cw.b * d + cw.m;
+        va[q] = (f < total && within < len)
+                    ? *reinterpret_cast<const float4*>(xb + (size_t)cw.a * x_row + within)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        cw.next(LIN_KC, d);
+      }
     }
-    if (src.k & 1) {  // odd K: the upper half-wave (k index k_even+1) contributes zero
-      const bool ok = kh == 0;
-      const float a = (ok && rok) ? xa[(k_even >> 1) * xs] : 0.0f;
-      const float b = (ok && jok) ? wb[(k_even >> 1) * ws] * al : 0.0f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-    }
-  }
-  if (!jok) return;
-  const float bj = (sl.bias_off >= 0) ? bias[sl.bias_off + j] : 0.0f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int rr = tile0 + (i & 3) + 8 * (i >> 2) + 4 * kh;
-    if (rr < rows) {
-      const int nn = rr / d, mm = rr - nn * d;
-      y[(size_t)nn * y_row + sl.y_off + j * d + mm] = acc[i] + bj;
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      const int k = e >> 5, jj = jt * 32 + (e & 31);
+      vb[q] = (k < kk && jj < sl.n_out) ? w[ch.w_off + (size_t)(ch.kc + k) * ch.ldk + (size_t)jj * ch.ldj] * ch.alpha
+                                        : 0.0f;
+    }
+  };
+  // write the staged registers of chunk c to LDS (scalar path: load + store directly)
+  auto store_chunk = [&](int c, bool with_a) {
+    if (with_a) {
+      if (vec) {
+        Walk3 cw;
+        cw.init(4 * tid, 4 * 256, LIN_KC, d);
+#pragma unroll
+        for (int q = 0; q < LIN_NV; ++q) {
+          const int f = 4 * tid + 1024 * q;
+          if (f < total) {
+            int k = cw.b, m = cw.m;
+            const int rbase = (n_lo + cw.a) * d - r0;
+            const float vv[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int row = rbase + m;
+              if (row >= 0 && row < LIN_ROWS) As[row * LIN_ST + k] = vv[t];
+              if (++m == d) { m = 0; ++k; }
+            }
+          }
+          cw.next(LIN_KC, d);
+        }
+      } else {
+        const ChunkRef ch = lin_chunk(sl, c);
+        const int kk = min(LIN_KC, ch.k - ch.kc);
+        const float* __restrict__ xb = x + (size_t)n_lo * x_row + ch.x_off + (size_t)ch.kc * d;
+        Walk3 cw;
+        cw.init(tid, 256, LIN_KC, d);
+        for (int f = tid; f < total; f += 256) {
+          const int row = (n_lo + cw.a) * d + cw.m - r0;
+          if (row >= 0 && row < LIN_ROWS)
+            As[row * LIN_ST + cw.b] = (cw.b < kk) ? xb[(size_t)cw.a * x_row + cw.b * d + cw.m] : 0.0f;
+          cw.next(LIN_KC, d);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      Bs[(e >> 5) * LIN_ST + (e & 31)] = vb[q];
+    }
+  };
+
+  const float* __restrict__ ar = As + (wave * 32 + (lane & 31)) * LIN_ST + (lane >> 5);
+  const float* __restrict__ br = Bs + (lane >> 5) * LIN_ST + (lane & 31);
+  for (int jt = 0; jt < n_jt; ++jt) {
+    eelg_f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    const bool restage = n_chunks > 1 || jt == 0;
+    load_chunk(0, jt, restage);
+    for (int c = 0; c < n_chunks; ++c) {
+      __syncthreads();  // previous MFMA reads of As / Bs and epilogue reads of Os are done
+      store_chunk(c, restage);
+      __syncthreads();
+      if (c + 1 < n_chunks) load_chunk(c + 1, jt, true);  // in flight during the MFMAs
+      // K padded to 32 with zeros (A and B) -> always 16 steps
+#pragma unroll
+      for (int st = 0; st < 16; ++st)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * st], br[2 * st * LIN_ST], acc, 0, 0, 0);
+    }
+    // epilogue: stage the 128 x 32 tile, then write per-node contiguous runs
+    const int j = jt * 32 + (lane & 31);
+    const float bj = (sl.bias_off >= 0 && j < sl.n_out) ? bias[sl.bias_off + j] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      Os[row * LIN_ST + (lane & 31)] = acc[i] + bj;
+    }
+    __syncthreads();
+    const int jw = min(32, sl.n_out - jt * 32);
+    const int olen = jw * d;  // floats per node in this column tile
+    float* __restrict__ yb = y + (size_t)n_lo * y_row + sl.y_off + (size_t)jt * 32 * d;
+    Walk3 ow;
+    ow.init(tid, 256, jw, d);
+    for (int f = tid; f < span * olen; f += 256) {
+      const int row = (n_lo + ow.a) * d + ow.m - r0;
+      if (row >= 0 && row < LIN_ROWS) yb[(size_t)ow.a * y_row + ow.b * d + ow.m] = Os[row * LIN_ST + ow.b];
+      ow.next(jw, d);
     }
   }
 }
 
 // grad W for each instruction: partial[p, w_off + u*n_out + j] =
-//   alpha * sum_{rows of this wave's slice} x[n, x_off + u*d + m] * g[n, g_off + j*d + m]
+//   alpha * sum_{nodes of slice p, m} x[n, x_off + u*d + m] * g[n, g_off + j*d + m]
+// One workgroup = (node slice, instruction, 32x32 (u, j) tile).  The four waves take
+// chunks of floor(32/d) whole nodes round-robin, stage their X[row][u] / G[row][j] tiles
+// (node-contiguous 32*d-float runs) in wave-private LDS, reduce over rows with MFMA
+// (zero-padded to 32 rows), and the four accumulators are summed through LDS at the end.
 __global__ __launch_bounds__(256) void lin_bwdw_kernel(const float* __restrict__ x, int x_row,
                                                        const float* __restrict__ g, int g_row,
-                                                       int n_nodes, int rows_per_wave,
+                                                       int n_nodes, int nodes_per_slice,
                                                        float* __restrict__ partial, int w_total,
                                                        eelg_linw_desc desc) {
+  __shared__ float Xs[4][32 * LIN_ST];
+  __shared__ float Gs[4][32 * LIN_ST];
   const eelg_linw_ins& in = desc.ins[blockIdx.y];
-  const int d = in.d;
-  const int rows = n_nodes * d;
-  const int n_ut = (in.k + 31) / 32;
-  const int uti = blockIdx.z / desc.max_jt, jti = blockIdx.z % desc.max_jt;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int slice = blockIdx.x * 4 + wave;
-  float* __restrict__ dst = partial + (size_t)slice * w_total + in.w_off;
-  if (uti >= n_ut || jti * 32 >= in.n_out) return;
-  const int kh = lane >> 5;
-  const int u = uti * 32 + (lane & 31);
-  const int j = jti * 32 + (lane & 31);
-  const bool uok = u < in.k, jok = j < in.n_out;
+  const int d = in.d, K = in.k, NO = in.n_out;
+  const int n_ut = (K + 31) / 32, n_jt = (NO + 31) / 32;
+  const int t = blockIdx.z;
+  if (t >= n_ut * n_jt) return;  // uniform per workgroup
+  const int ut = t / n_jt, jt = t - ut * n_jt;
+  const int uw = min(32, K - ut * 32), jw = min(32, NO - jt * 32);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int slice = blockIdx.x;
+  const int n0 = slice * nodes_per_slice;
+  const int n1 = min(n_nodes, n0 + nodes_per_slice);
+  const int nb = 32 / d;  // whole nodes per chunk
+  float* __restrict__ xs = Xs[wave];
+  float* __restrict__ gs = Gs[wave];
+  // pad rows [nb*d, 32) stay zero for the whole kernel
+  for (int f = lane; f < (32 - nb * d) * LIN_ST; f += 64) {
+    xs[nb * d * LIN_ST + f] = 0.0f;
+    gs[nb * d * LIN_ST + f] = 0.0f;
+  }
   eelg_f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-  const int r0 = slice * rows_per_wave;
-  const int r1 = min(rows, r0 + rows_per_wave);
-  if (r0 < r1) {
-    // this lane walks rows r0 + kh, r0 + kh + 2, ...
-    int r = r0 + kh;
-    int n = r / d, m = r - n * d;
-    const float* __restrict__ xb = x + in.x_off + (size_t)u * d;
-    const float* __restrict__ gb = g + in.g_off + (size_t)j * d;
-    for (; r - kh < r1; r += 2) {
-      const bool ok = r < r1;
-      const float a = (ok && uok) ? xb[(size_t)n * x_row + m] : 0.0f;
-      const float b = (ok && jok) ? gb[(size_t)n * g_row + m] : 0.0f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      m += 2;
-      if (m >= d) { m -= d; ++n; if (m >= d) { m -= d; ++n; } }
-    }
-  }
-  if (!jok) return;
+  const float* __restrict__ xb = x + in.x_off + (size_t)ut * 32 * d;
+  const float* __restrict__ gb = g + in.g_off + (size_t)jt * 32 * d;
+  // register-staged chunk: lane owns flat entries f = lane + 64 q (q < 16) of the
+  // (node, channel, m) runs of <= nb whole nodes; the next chunk's loads are issued
+  // before the current chunk's MFMAs
+  float rx[16], rg[16];
+  auto load_chunk = [&](int nc) {
+    const int cn = min(nb, n1 - nc);
+    Walk3 w3;
+    w3.init(lane, 64, 32, d);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int uu = uti * 32 + (i & 3) + 8 * (i >> 2) + 4 * kh;
-    if (uu < in.k) dst[uu * in.n_out + j] = acc[i] * in.alpha;
+    for (int q = 0; q < 16; ++q) {
+      const bool in_node = w3.a < cn;
+      rx[q] = (in_node && w3.b < uw) ? xb[(size_t)(nc + w3.a) * x_row + w3.b * d + w3.m] : 0.0f;
+      rg[q] = (in_node && w3.b < jw) ? gb[(size_t)(nc + w3.a) * g_row + w3.b * d + w3.m] : 0.0f;
+      w3.next(32, d);
+    }
+  };
+  const int flat = nb * 32 * d;  // <= 1024 entries per chunk
+  int nc = n0 + wave * nb;
+  if (nc < n1) load_chunk(nc);
+  for (; nc < n1; nc += 4 * nb) {
+    {
+      Walk3 w3;
+      w3.init(lane, 64, 32, d);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (lane + 64 * q < flat) {
+          const int row = w3.a * d + w3.m;
+          xs[row * LIN_ST + w3.b] = rx[q];
+          gs[row * LIN_ST + w3.b] = rg[q];
+        }
+        w3.next(32, d);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (nc + 4 * nb < n1) load_chunk(nc + 4 * nb);
+    const float* __restrict__ xr = xs + (lane >> 5) * LIN_ST + (lane & 31);
+    const float* __restrict__ gr = gs + (lane >> 5) * LIN_ST + (lane & 31);
+#pragma unroll
+    for (int st = 0; st < 16; ++st)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[2 * st * LIN_ST], gr[2 * st * LIN_ST], acc, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+  }
+  // cross-wave reduction through LDS (reuse Xs: 4 x 32*33 >= 3 x 16*64 floats)
+  __syncthreads();
+  float* red = &Xs[0][0];
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[((wave - 1) * 16 + i) * 64 + lane] = acc[i];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* __restrict__ dst = partial + (size_t)slice * w_total + in.w_off;
+    const int j = jt * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i] + red[i * 64 + lane] + red[(16 + i) * 64 + lane] + red[(32 + i) * 64 + lane];
+      const int uu = ut * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      if (uu < K && j < NO) dst[(size_t)uu * NO + j] = v * in.alpha;
+    }
   }
 }

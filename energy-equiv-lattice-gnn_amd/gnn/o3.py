@@ -123,6 +123,8 @@ class Linear(torch.nn.Module):
             e.n_out, e.d, e.w_off, e.alpha = self.irreps_out[o].mul, self.irreps_in[i].ir.dim, wo, a
         self._bw_desc = wd
         self._bw_maxd = max([self.irreps_in[i].ir.dim for i, _ in self.instructions] or [1])
+        self._bw_tiles = sum(((self.irreps_in[i].mul + 31) // 32) * ((self.irreps_out[o].mul + 31) // 32)
+                             for i, o in self.instructions) or 1
 
     # -- launches ---------------------------------------------------------------
     def _fwd(self, x, weight, bias):
@@ -150,15 +152,15 @@ class Linear(torch.nn.Module):
         n = x.shape[0]
         if not self.instructions:
             return torch.zeros_like(self.weight)
-        max_rows = n * self._bw_maxd
-        rpw = max(256, min(4096, (max_rows // 1024 + 1) // 2 * 2))
-        slices = (max_rows + rpw - 1) // rpw
-        n_part = (slices + 3) // 4 * 4
-        self._bw_desc.max_rows = max_rows
-        part = torch.empty(n_part, self.weight_numel, device=x.device, dtype=torch.float32)
+        # ~2048 workgroups in total: (node slices) x (32x32 weight tiles of all instructions)
+        slices = max(1, min((n + 31) // 32, -(-2048 // self._bw_tiles)))
+        nps = -(-n // slices)
+        slices = -(-n // nps)
+        self._bw_desc.max_rows = n * self._bw_maxd
+        part = torch.empty(slices, self.weight_numel, device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().eelg_linear_bwd_w(
-            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, rpw,
-            _lib.ptr(part), n_part, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream()),
+            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, nps,
+            _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream()),
             "linear_bwd_w")
         return part.sum(0)
 

@@ -96,13 +96,14 @@ typedef struct { int n_slots, max_jt, max_rows, pad; eelg_lin_slot slot[EELG_LIN
 int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
                     float* y, int y_row, const eelg_lin_desc* desc, void* stream);
 
-/* grad of the weights: partial[p, w_off + u*n_out + j] over row slices p (sum over p
- * on the caller side; deterministic).  n_partial must be >= 4*ceil(max_slices/4). */
+/* grad of the weights: partial[p, w_off + u*n_out + j] over node slices p of
+ * nodes_per_slice nodes (sum over p on the caller side; deterministic).
+ * n_partial must be >= ceil(n_nodes / nodes_per_slice). */
 #define EELG_LINW_MAXINS 8
 typedef struct { int x_off, k, g_off, n_out, d, w_off; float alpha; } eelg_linw_ins;
 typedef struct { int n_ins, max_jt, max_ut, max_rows; eelg_linw_ins ins[EELG_LINW_MAXINS]; } eelg_linw_desc;
 int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,
-                      int rows_per_wave, float* partial, int n_partial, int w_total,
+                      int nodes_per_slice, float* partial, int n_partial, int w_total,
                       const eelg_linw_desc* desc, void* stream);
 
 #ifdef __cplusplus
