@@ -196,7 +196,7 @@ class TensorProductInteractionBlock(torch.nn.Module):
         csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
         idx, info = self._config()
         x = self.linear_up(node_feats)
-        w = self.conv_tp_weights(edge_feats)
+        w = ops.radial_mlp(edge_feats, self.conv_tp_weights)
         agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
         return self.linear(agg), None
 

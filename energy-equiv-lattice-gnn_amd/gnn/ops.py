@@ -265,3 +265,81 @@ class _SymCon(torch.autograd.Function):
 def symmetric_contraction(x, coef, cfg: int, info: Dict[str, int], mul: int):
     _require_device(x, coef)
     return _SymCon.apply(x, coef, cfg, info, mul)
+
+
+# ---------------------------------------------------------------------------
+# radial MLP (conv_tp_weights, gnn/blocks.py:537-549)
+# ---------------------------------------------------------------------------
+def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
+    """g^T @ x over a long row dimension as a split-K batched GEMM + fixed-order sum
+    (library GEMMs pick no split-K for [64 x 131072] @ [131072 x 64] and run on a few CUs)."""
+    e = g.shape[0]
+    c = e // chunk
+    out = None
+    if c > 1:
+        m = c * chunk
+        out = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2), x[:m].view(c, chunk, -1)).sum(0)
+        g, x = g[m:], x[m:]
+    if g.shape[0]:
+        rest = g.t() @ x
+        out = rest if out is None else out + rest
+    return out if out is not None else torch.zeros(g.shape[1], x.shape[1], device=g.device, dtype=g.dtype)
+
+
+class _RadialMLP(torch.autograd.Function):
+    """Linear(+bias)-SiLU-...-Linear(no bias) on edge features (no grad w.r.t. the
+    features, which come from eelg_edge_embed without grad).  Saves the
+    pre-activations; weight gradients use the split-K form above."""
+
+    @staticmethod
+    def forward(ctx, feats, *params):
+        n_hidden = (len(params) - 1) // 2
+        h, zs, hs = feats, [], [feats]
+        for i in range(n_hidden):
+            z = torch.addmm(params[2 * i + 1], h, params[2 * i].t())
+            h = torch.nn.functional.silu(z)
+            zs.append(z)
+            hs.append(h)
+        out = h @ params[-1].t()
+        ctx.save_for_backward(*params, *zs, *hs)
+        ctx.n_hidden = n_hidden
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        n = ctx.n_hidden
+        saved = ctx.saved_tensors
+        params = saved[: 2 * n + 1]
+        zs = saved[2 * n + 1: 3 * n + 1]
+        hs = saved[3 * n + 1:]
+        g = g.contiguous()
+        grads = [None] * len(params)
+        grads[-1] = _wgrad(g, hs[-1])                      # [W, hidden]
+        gh = g @ params[-1]
+        for i in range(n - 1, -1, -1):
+            gz = torch.ops.aten.silu_backward(gh, zs[i])
+            grads[2 * i] = _wgrad(gz, hs[i])
+            grads[2 * i + 1] = gz.sum(0)
+            if i > 0:
+                gh = gz @ params[2 * i]
+        return (None, *grads)
+
+
+def radial_mlp(feats: torch.Tensor, mlp: torch.nn.Sequential) -> torch.Tensor:
+    """Apply ``mlp`` = [Linear(bias), SiLU]*k + [Linear(no bias)] with the fused backward."""
+    mods = list(mlp)
+    params = []
+    for i, mod in enumerate(mods):
+        if isinstance(mod, torch.nn.Linear):
+            last = i == len(mods) - 1
+            if last != (mod.bias is None):
+                raise ValueError("radial MLP: expected biases on hidden layers only")
+            params.append(mod.weight)
+            if not last:
+                params.append(mod.bias)
+        elif not isinstance(mod, torch.nn.SiLU):
+            raise ValueError(f"radial MLP: unsupported module {type(mod).__name__}")
+    tok = TIMER.start("radial_mlp_fwd")
+    out = _RadialMLP.apply(_f32(feats), *params)
+    TIMER.stop(tok)
+    return out

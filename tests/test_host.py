@@ -172,3 +172,35 @@ def test_product_model_param_names_match_oracle():
     po = {k: v.shape for k, v in o.named_parameters()}
     assert pm == po
     assert sum(v.numel() for v in m.parameters()) == 223186
+
+
+@pytest.mark.parametrize("e", [7, 1500])
+def test_radial_mlp_matches_sequential_autograd(e):
+    """ops.radial_mlp (split-K weight grads, saved pre-activations) == nn.Sequential autograd."""
+    from gnn import ops
+    torch.manual_seed(0)
+    mlp = torch.nn.Sequential(torch.nn.Linear(12, 16), torch.nn.SiLU(), torch.nn.Linear(16, 16),
+                              torch.nn.SiLU(), torch.nn.Linear(16, 40, bias=False)).double()
+    f = torch.randn(e, 12, dtype=torch.float64)
+    g = torch.randn(e, 40, dtype=torch.float64)
+    (mlp(f) * g).sum().backward()
+    ref = {k: p.grad.clone() for k, p in mlp.named_parameters()}
+    out_ref = mlp(f).detach()
+    mlp.zero_grad()
+    orig = ops._f32
+    ops._f32 = lambda t: t.contiguous()          # fp64 on CPU for the check
+    try:
+        out = ops.radial_mlp(f, mlp)
+        (out * g).sum().backward()
+    finally:
+        ops._f32 = orig
+    assert torch.allclose(out, out_ref, atol=1e-12)
+    for k, p in mlp.named_parameters():
+        assert torch.allclose(p.grad, ref[k], atol=1e-10), k
+
+
+def test_wgrad_split_k_matches_matmul():
+    from gnn.ops import _wgrad
+    g = torch.randn(1300, 8, dtype=torch.float64)
+    x = torch.randn(1300, 5, dtype=torch.float64)
+    assert torch.allclose(_wgrad(g, x, chunk=256), g.t() @ x, atol=1e-10)
