@@ -24,7 +24,7 @@ from __future__ import annotations
 import math
 import os
 import sys
-from typing import Dict, List, Tuple
+from typing import Sequence, Dict, List, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
@@ -294,15 +294,49 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
 # ---------------------------------------------------------------------------
 # symmetric contraction
 # ---------------------------------------------------------------------------
-def pin(vs: List[str], memory: bool = False) -> str:
-    """Empty asm that 'modifies' every listed register and clobbers memory: a hard
-    boundary for the scheduler, so each term group computes in place (without it
-    hipcc hoists thousands of monomials / scalar coefficient loads and spills)."""
+def pin(vs: List[str], memory: bool = False, sgprs: Sequence[str] = ()) -> str:
+    """Empty asm that 'modifies' every listed register: a hard boundary for the
+    scheduler, so each term block computes in place (without it hipcc hoists
+    thousands of monomials / scalar coefficient loads and spills).  ``sgprs`` are
+    wave-uniform values forced to be resident (loaded) at this point."""
     out = []
-    for k in range(0, len(vs), 10):
-        ops = ", ".join(f'"+v"({v})' for v in vs[k: k + 10])
+    ops_all = [f'"+v"({v})' for v in vs] + [f'"+s"({v})' for v in sgprs]
+    for k in range(0, len(ops_all), 10):
+        ops = ", ".join(ops_all[k: k + 10])
         out.append(f'asm volatile("" : {ops}{" : : " + chr(34) + "memory" + chr(34) if memory else ""});')
     return " ".join(out)
+
+
+def sc_blocks(plan, maxb: int = 32) -> List[Dict]:
+    """Split the polynomial terms into blocks of <= maxb terms (one (a, b) group may span
+    several blocks; a c-subgroup is never split).  Each block's coefficients are
+    prefetched into SGPRs while the previous block computes."""
+    deg1, pairs = [], {}
+    for t, (nu, (a, b, c), q) in enumerate(plan.terms):
+        if nu == 1:
+            deg1.append((t, a, q))
+        else:
+            g = pairs.setdefault((a, b), {"d2": [], "d3": {}})
+            if nu == 2:
+                g["d2"].append((t, q))
+            else:
+                g["d3"].setdefault(c, []).append((t, q))
+    blocks = []
+    if deg1:
+        blocks.append({"kind": "deg1", "terms": [t for t, _, _ in deg1], "deg1": deg1})
+    for (a, b), g in pairs.items():
+        cur = {"kind": "pair", "a": a, "b": b, "first": True, "last": False,
+               "d2": list(g["d2"]), "d3": [], "terms": [t for t, _ in g["d2"]]}
+        for c, lst in g["d3"].items():
+            if cur["terms"] and len(cur["terms"]) + len(lst) > maxb:
+                blocks.append(cur)
+                cur = {"kind": "pair", "a": a, "b": b, "first": False, "last": False,
+                       "d2": [], "d3": [], "terms": []}
+            cur["d3"].append((c, lst))
+            cur["terms"] += [t for t, _ in lst]
+        cur["last"] = True
+        blocks.append(cur)
+    return blocks
 
 
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
@@ -409,19 +443,33 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     for q in range(D):
         L.append(f"  float o{q} = 0.0f;")
     fpin = pin([f"x{a}" for a in range(D)] + [f"o{q}" for q in range(D)])
-    for t, a, q in deg1:
-        L.append(f"  o{q} = fmaf(cf[{t}], x{a}, o{q});")
-    for (a, b), g in pairs.items():
-        L.append(f"  {{ const float p = x{a} * x{b};")
-        for t, q in g["d2"]:
-            L.append(f"    o{q} = fmaf(cf[{t}], p, o{q});")
-        for cc, lst in g["d3"].items():
-            L.append(f"    {{ const float m = p * x{cc};")
-            for t, q in lst:
-                L.append(f"      o{q} = fmaf(cf[{t}], m, o{q});")
-            L.append("    }")
-        L.append("  }")
-        L.append("  " + fpin)
+    blocks = sc_blocks(plan)
+    fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(D)]
+    for t in blocks[0]["terms"]:
+        L.append(f"  float c{t} = cf[{t}];")
+    for bi, blk in enumerate(blocks):
+        nxt = blocks[bi + 1]["terms"] if bi + 1 < len(blocks) else []
+        for t in nxt:
+            L.append(f"  float c{t} = cf[{t}];")
+        carry = []
+        if blk["kind"] == "deg1":
+            for t, a, q in blk["deg1"]:
+                L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
+        else:
+            a, b = blk["a"], blk["b"]
+            pv = f"p{a}_{b}"
+            if blk["first"]:
+                L.append(f"  float {pv} = x{a} * x{b};")
+            for t, q in blk["d2"]:
+                L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
+            for cc, lst in blk["d3"]:
+                L.append(f"  {{ const float m = {pv} * x{cc};")
+                for t, q in lst:
+                    L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
+                L.append("  }")
+            if not blk["last"]:
+                carry = [pv]
+        L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for q in range(D):
         L.append(f"  tr[{lq(q, 'cl')}] = o{q};")
@@ -447,19 +495,34 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     for q in range(D):
         L.append(f"  float g{q} = gr[{lq(q, 'cl')}];")
     bpin = pin([f"x{a}" for a in range(D)] + [f"g{q}" for q in range(D)] + [f"d{a}" for a in range(D)])
-    for t, a, q in deg1:
-        L.append(f"  d{a} = fmaf(cf[{t}], g{q}, d{a});")
-    for (a, b), g in pairs.items():
-        L.append(f"  {{ const float p = x{a} * x{b}; float s2 = 0.0f;")
-        for t, q in g["d2"]:
-            L.append(f"    s2 = fmaf(cf[{t}], g{q}, s2);")
-        for cc, lst in g["d3"].items():
-            L.append("    { float s = 0.0f;")
-            for t, q in lst:
-                L.append(f"      s = fmaf(cf[{t}], g{q}, s);")
-            L.append(f"      d{cc} = fmaf(s, p, d{cc}); s2 = fmaf(s, x{cc}, s2); }}")
-        L.append(f"    d{a} = fmaf(s2, x{b}, d{a}); d{b} = fmaf(s2, x{a}, d{b}); }}")
-        L.append("  " + bpin)
+    bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(D)] + [f"d{a}" for a in range(D)]
+    for t in blocks[0]["terms"]:
+        L.append(f"  float c{t} = cf[{t}];")
+    for bi, blk in enumerate(blocks):
+        nxt = blocks[bi + 1]["terms"] if bi + 1 < len(blocks) else []
+        for t in nxt:
+            L.append(f"  float c{t} = cf[{t}];")
+        carry = []
+        if blk["kind"] == "deg1":
+            for t, a, q in blk["deg1"]:
+                L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
+        else:
+            a, b = blk["a"], blk["b"]
+            pv, sv = f"p{a}_{b}", f"s{a}_{b}"
+            if blk["first"]:
+                L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
+            for t, q in blk["d2"]:
+                L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
+            for cc, lst in blk["d3"]:
+                L.append("  { float s = 0.0f;")
+                for t, q in lst:
+                    L.append(f"    s = fmaf(c{t}, g{q}, s);")
+                L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
+            if blk["last"]:
+                L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
+            else:
+                carry = [pv, sv]
+        L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for a in range(D):
         L.append(f"  xr[{lq(a, 'cl')}] = d{a};")
@@ -528,14 +591,24 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                        f" else {{ rx{it} = 0.0f; rg{it} = 0.0f; }} }}")
         return out
     L += issue("nb")
-    L.append("  for (int n0 = nb; n0 < ne; n0 += 64) {")
-    for it in range(per):
-        L.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) {{ sx[idx] = rx{it}; sg[idx] = rg{it}; }} }}")
-    L.append("    __syncthreads();")
-    L.append("    if (n0 + 64 < ne) {")
-    L += issue("n0 + 64")
-    L.append("    }")
-    L.append("    switch (jg) {")
+
+    def tile_loop(body):
+        """the 64-node tile loop; every wave of the workgroup runs it (same barrier count)"""
+        out = ["      for (int n0 = nb; n0 < ne; n0 += 64) {"]
+        for it in range(per):
+            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) {{ sx[idx] = rx{it}; sg[idx] = rg{it}; }} }}")
+        out.append("        __syncthreads();")
+        out.append("        if (n0 + 64 < ne) {")
+        out += ["    " + ln for ln in issue("n0 + 64")]
+        out.append("        }")
+        out += body
+        out.append("        __syncthreads();")
+        out.append("      }")
+        return out
+
+    # each case owns its tile loop, so the 64 accumulators stay in place across tiles
+    # (a switch inside the loop merges them every iteration: 64 v_mov per tile)
+    L.append("  switch (jg) {")
     for gi, grp in enumerate(groups):
         L.append(f"    case {gi}: {{")
         need_x, need_g = set(), set()
@@ -547,33 +620,36 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 need_x.add(b)
             if nu >= 3:
                 need_x.add(cc)
+        body = []
         for a in sorted(need_x):
-            L.append(f"      const float x{a} = sx[{a * 64} + lane];")
+            body.append(f"        const float x{a} = sx[{a * 64} + lane];")
         for q in sorted(need_g):
-            L.append(f"      const float g{q} = sg[{q * 64} + lane];")
+            body.append(f"        const float g{q} = sg[{q * 64} + lane];")
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         cur = None
         for jj, t in enumerate(grp):
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
-                L.append(f"      acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
+                body.append(f"        acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
                 continue
             if cur != (a, b):
                 if cur is not None:
-                    L.append("      }")
-                    L.append("      " + cpin)
-                L.append(f"      {{ const float p = x{a} * x{b};")
+                    body.append("        }")
+                    body.append("        " + cpin)
+                body.append(f"        {{ const float p = x{a} * x{b};")
                 cur = (a, b)
             if nu == 2:
-                L.append(f"        acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
+                body.append(f"          acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
             else:
-                L.append(f"        acc[{jj}] = fmaf(p * x{cc}, g{q}, acc[{jj}]);")
+                body.append(f"          acc[{jj}] = fmaf(p * x{cc}, g{q}, acc[{jj}]);")
         if cur is not None:
-            L.append("      }")
+            body.append("        }")
+        body.append("        " + cpin)
+        L += tile_loop(body)
         L.append("      break; }")
-    L.append("    default: break;")
-    L.append("    }")
-    L.append("    __syncthreads();")
+    L.append("    default: {")
+    L += tile_loop([])
+    L.append("      break; }")
     L.append("  }")
     # recursive-halving reduction over the 6 lane bits: with R = JG / 64 values left
     # per lane, lane L ends with terms R*L + i (i < R)
