@@ -187,28 +187,44 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         for p in grp:
             for k in range(2 * p.l3 + 1):
                 L.append(f"    float a{p.slot}_{k} = 0.0f;")
+        # software-pipelined edge loop: the next edge's sender -> x gather, SH row and
+        # weights are in flight while the current edge computes
+        cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
+               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+               + [f"w{p.slot}" for p in grp])
+
+        def load(pref, ev, guard):
+            out = [f"    {{ const bool ok = {guard};",
+                   f"      const float* __restrict__ xs = x + (size_t)(ok ? sender[{ev}] : 0) * {din};",
+                   f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nsh};",
+                   f"      const float* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
+            for l in need_l1:
+                d = 2 * l + 1
+                for i in range(d):
+                    out.append(f"      {pref}x{l}_{i} = ok ? xs[{node_off[l]} + u * {d} + {i}] : 0.0f;")
+            for l in need_l2:
+                for j in range(2 * l + 1):
+                    out.append(f"      {pref}y{l * l + j} = ok ? ye[{l * l + j}] : 0.0f;")
+            for p in grp:
+                out.append(f"      {pref}w{p.slot} = ok ? we[{p.slot * MUL}] : 0.0f;")
+            out.append("    }")
+            return out
+        L.append("    float " + ", ".join(cur) + ";")
+        L += load("", "beg", "beg < end")
         L.append("    for (int e = beg; e < end; ++e) {")
-        L.append("      const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
-        L.append("      const float* __restrict__ ye = sh + (size_t)e * " + str(nsh) + ";")
-        L.append("      const float* __restrict__ we = w + (size_t)e * " + str(wn) + " + u;")
-        for l in need_l1:
-            d = 2 * l + 1
-            for i in range(d):
-                L.append(f"      float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
-        for l in need_l2:
-            for j in range(2 * l + 1):
-                L.append(f"      float y{l * l + j} = ye[{l * l + j}];")
-        gpin = pin([f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
-                   + [f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
-                   + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)])
+        L.append("      float " + ", ".join("n" + v for v in cur) + ";")
+        L += ["  " + ln for ln in load("n", "e + 1", "e + 1 < end")]
+        gpin = pin([f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)] + cur
+                   + ["n" + v for v in cur])
         for p in grp:
             L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-            L.append(f"        const float wp = we[{p.slot * MUL}] * ({flit(p.coef)} * inv_norm);")
+            L.append(f"        const float wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
             _emit_t(p, xname, yname, "t", L, "        ")
             for k in range(2 * p.l3 + 1):
                 L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
             L.append("      }")
             L.append("      " + gpin)
+        L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
         L.append("    }")
         for p in grp:
             d3 = 2 * p.l3 + 1
