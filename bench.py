@@ -146,7 +146,7 @@ def main():
     allreduce = FlatGradAllReduce(plist)
 
     def step():
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         loss = stiffness_loss(model(batch)["stiffness"], batch.stiffness)
         loss.backward()
         allreduce()                      # one flat fp32 RCCL all-reduce (no-op at N=1)

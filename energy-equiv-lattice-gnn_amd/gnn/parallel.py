@@ -25,40 +25,31 @@ def shard_indices(num_items: int, rank: int, world: int, per_rank: int, step: in
 
 
 class FlatGradAllReduce:
-    """One flat buffer for all gradients; ``__call__`` all-reduces and averages them."""
+    """One flat buffer for all gradients; ``__call__`` all-reduces and averages them.
+
+    Packing is one ``torch.cat`` and unpacking one ``_foreach_copy_`` (a handful of
+    launches instead of two copies per parameter), so the exchange costs one RCCL
+    all-reduce plus O(1) kernels per step.  Missing gradients count as zeros."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         self.numel = sum(p.numel() for p in self.params)
-        dev = self.params[0].device if self.params else torch.device("cpu")
-        self.flat = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         self.group = group
 
     def __call__(self) -> None:
         if not dist.is_available() or not dist.is_initialized():
             return
         world = dist.get_world_size(self.group)
-        if world == 1:
+        if world == 1 or not self.params:
             return
-        off = 0
         for p in self.params:
-            n = p.numel()
             if p.grad is None:
-                self.flat[off: off + n].zero_()
-            else:
-                self.flat[off: off + n].copy_(p.grad.reshape(-1))
-            off += n
-        dist.all_reduce(self.flat, group=self.group)
-        self.flat.div_(world)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            g = self.flat[off: off + n].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            off += n
+                p.grad = torch.zeros_like(p)
+        grads = [p.grad for p in self.params]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, group=self.group)
+        flat.div_(world)
+        torch._foreach_copy_(grads, [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)])
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:
