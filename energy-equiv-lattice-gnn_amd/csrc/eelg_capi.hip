@@ -103,6 +103,63 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
   }
 }
 
+// Few long segments (graph pooling: 32 graphs x 1024 nodes): split each segment into
+// n_split contiguous pieces, one wave per (segment, piece) -> work[seg][piece][:], then
+// a fixed-order combine.  Deterministic, no atomics.
+__global__ __launch_bounds__(256) void segment_split_kernel(
+    const float* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ idx,
+    int n_rows, int width, int n_split, float* __restrict__ work) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wid >= n_rows * n_split) return;
+  const int row = wid / n_split, sp = wid - row * n_split;
+  const int b0 = rowptr[row], len = rowptr[row + 1] - b0;
+  const int beg = b0 + (int)(((long long)len * sp) / n_split);
+  const int end = b0 + (int)(((long long)len * (sp + 1)) / n_split);
+  float* __restrict__ o = work + (size_t)wid * width;
+  for (int c = lane; c < width; c += 64) {
+    float acc = 0.f;
+    for (int j = beg; j < end; ++j) {
+      const int sr = idx ? idx[j] : j;
+      acc += src[(size_t)sr * width + c];
+    }
+    o[c] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void segment_combine_kernel(
+    const float* __restrict__ work, const float* __restrict__ row_scale, float scale, int n_rows,
+    int width, int n_split, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_rows * width) return;
+  const int row = i / width, c = i - row * width;
+  const float* __restrict__ w = work + (size_t)row * n_split * width + c;
+  float acc = 0.f;
+  for (int s = 0; s < n_split; ++s) acc += w[(size_t)s * width];
+  out[i] = acc * scale * (row_scale ? row_scale[row] : 1.0f);
+}
+
+// Sparse (CSR) x dense with strided operands: out[r, c] = sum_j val[j] * B[col[j], c].
+// Four lanes per (r, c) (c fastest across lane quads) split a row's nonzeros and are
+// combined with two xor-shuffles in a fixed order, so long rows (U_sym^T: ~120 nnz) do
+// not serialise one dependent chain.
+__global__ __launch_bounds__(256) void csr_spmm_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
+    int n_rows, const float* __restrict__ B, int ldb_r, int ldb_c, int n_cols,
+    float* __restrict__ out, int ldo_r, int ldo_c) {
+  const int gi = blockIdx.x * 256 + threadIdx.x;
+  const int sub = gi & 3, i = gi >> 2;
+  const bool ok = i < n_rows * n_cols;
+  const int r = ok ? i / n_cols : 0, c = ok ? i - r * n_cols : 0;
+  float acc = 0.f;
+  if (ok)
+    for (int j = rowptr[r] + sub; j < rowptr[r + 1]; j += 4)
+      acc = fmaf(val[j], B[(size_t)col[j] * ldb_r + (size_t)c * ldb_c], acc);
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  if (ok && sub == 0) out[(size_t)r * ldo_r + (size_t)c * ldo_c] = acc;
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -199,6 +256,27 @@ int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
     hipLaunchKernelGGL(segment_sum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src,
                        rowptr, idx, row_scale, scale, n_rows, width, out);
   return check_launch("segment_sum_csr");
+}
+
+int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
+                           const float* row_scale, float scale, int n_rows, int width, int n_split,
+                           float* work, float* out, void* stream) {
+  if (n_rows <= 0 || width <= 0) return 0;
+  if (n_split <= 0) return fail(-2, "segment_sum_split: n_split must be positive");
+  hipLaunchKernelGGL(segment_split_kernel, dim3((n_rows * n_split + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, src, rowptr, idx, n_rows, width, n_split, work);
+  hipLaunchKernelGGL(segment_combine_kernel, dim3((n_rows * width + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, work, row_scale, scale, n_rows, width, n_split, out);
+  return check_launch("segment_sum_split");
+}
+
+int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_rows, const float* B,
+                  int ldb_r, int ldb_c, int n_cols, float* out, int ldo_r, int ldo_c, void* stream) {
+  if (n_rows <= 0 || n_cols <= 0) return 0;
+  hipLaunchKernelGGL(csr_spmm_kernel, dim3((4 * n_rows * n_cols + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, rowptr, col, val, n_rows, B, ldb_r, ldb_c, n_cols, out,
+                     ldo_r, ldo_c);
+  return check_launch("csr_spmm");
 }
 
 static const eelg_sc_cfg* sc_get(int cfg, int mul) {

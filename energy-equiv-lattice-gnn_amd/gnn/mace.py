@@ -81,7 +81,12 @@ class SymmetricContraction(torch.nn.Module):
         return torch.cat(ws, dim=0)                     # [K_total, mul]
 
     def coefficients(self) -> torch.Tensor:
-        return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()   # [mul, nterms]
+        """[mul, nterms] = (U_sym @ W)^T with the 1.6 %-dense U_sym applied as CSR on the GPU."""
+        if self.u_sym.is_cuda:
+            if getattr(self, "_u_csr", None) is None:
+                self._u_csr = ops.SparseRows(self.u_sym)
+            return ops.symcon_coefficients(self.weight_matrix(), self._u_csr)
+        return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idx, info = self._config()

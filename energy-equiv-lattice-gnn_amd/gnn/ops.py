@@ -133,13 +133,34 @@ def segment_sum_csr(src, rowptr, n_rows: int, idx=None, row_scale=None, scale: f
     return out
 
 
+def segment_sum_long(src: torch.Tensor, rowptr: torch.Tensor, n_rows: int,
+                     row_scale: Optional[torch.Tensor] = None, scale: float = 1.0) -> torch.Tensor:
+    """``segment_sum_csr`` for few long segments (graph pooling): each segment is split
+    into pieces summed in parallel, then combined in a fixed order (deterministic)."""
+    _require_device(src)
+    src = _f32(src)
+    width = src.shape[1]
+    n_split = max(1, min(64, -(-2048 // max(n_rows, 1))))
+    work = torch.empty(n_rows, n_split, width, device=src.device, dtype=torch.float32)
+    out = torch.empty(n_rows, width, device=src.device, dtype=torch.float32)
+    tok = TIMER.start("segment_sum_split")
+    _lib.check(_lib.load().eelg_segment_sum_split(
+        _lib.ptr(src), _lib.ptr(rowptr), None, _lib.ptr(row_scale), float(scale), n_rows, width,
+        n_split, _lib.ptr(work), _lib.ptr(out), _lib.stream()), "segment_sum_split")
+    TIMER.stop(tok)
+    return out
+
+
 class _SegmentMean(torch.autograd.Function):
     """Per-graph mean/sum pool over sorted ``batch`` (``gnn/model.py:100-106``)."""
 
     @staticmethod
     def forward(ctx, src, ptr32, batch, inv_cnt):
         ctx.save_for_backward(batch, inv_cnt)
-        return segment_sum_csr(src, ptr32, ptr32.shape[0] - 1, row_scale=inv_cnt)
+        n_rows = ptr32.shape[0] - 1
+        if src.shape[0] >= 64 * max(n_rows, 1):          # long segments: split them
+            return segment_sum_long(src, ptr32, n_rows, row_scale=inv_cnt)
+        return segment_sum_csr(src, ptr32, n_rows, row_scale=inv_cnt)
 
     @staticmethod
     def backward(ctx, g):
@@ -343,3 +364,65 @@ def radial_mlp(feats: torch.Tensor, mlp: torch.nn.Sequential) -> torch.Tensor:
     out = _RadialMLP.apply(_f32(feats), *params)
     TIMER.stop(tok)
     return out
+
+
+# ---------------------------------------------------------------------------
+# symmetric-contraction coefficients coef = (U_sym @ W)^T with a sparse U_sym
+# ---------------------------------------------------------------------------
+class SparseRows:
+    """CSR of a fixed matrix and of its transpose (device int32 / fp32)."""
+
+    def __init__(self, dense: torch.Tensor):
+        d = dense.detach().to(torch.float64).cpu()
+        self.shape = tuple(d.shape)
+        for name, m in (("a", d), ("t", d.t())):
+            nz = m != 0
+            rowptr = torch.zeros(m.shape[0] + 1, dtype=torch.int32)
+            rowptr[1:] = torch.cumsum(nz.sum(1), 0).to(torch.int32)
+            r, c = torch.nonzero(nz, as_tuple=True)
+            setattr(self, name, (rowptr, c.to(torch.int32), m[r, c].to(torch.float32)))
+        self._dev = {}
+
+    def on(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = tuple(tuple(t.to(device) for t in trip) for trip in (self.a, self.t))
+        return self._dev[key]
+
+
+def _spmm(trip, n_rows, B, ldb_r, ldb_c, n_cols, out, ldo_r, ldo_c):
+    rp, col, val = trip
+    _lib.check(_lib.load().eelg_csr_spmm(_lib.ptr(rp), _lib.ptr(col), _lib.ptr(val), n_rows,
+                                         _lib.ptr(B), ldb_r, ldb_c, n_cols, _lib.ptr(out), ldo_r,
+                                         ldo_c, _lib.stream()), "csr_spmm")
+
+
+class _SymConCoef(torch.autograd.Function):
+    """coef[c, t] = sum_k U[t, k] W[k, c]  ([mul, nterms], the layout the sc kernels read)."""
+
+    @staticmethod
+    def forward(ctx, w, sp: SparseRows):
+        _require_device(w)
+        w = _f32(w)
+        nt, nk = sp.shape
+        mul = w.shape[1]
+        a, t = sp.on(w.device)
+        coef = torch.empty(mul, nt, device=w.device, dtype=torch.float32)
+        _spmm(a, nt, w, mul, 1, mul, coef, 1, nt)                 # out[t, c] at c*nt + t
+        ctx.sp, ctx.mul = sp, mul
+        return coef
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _f32(g)
+        sp, mul = ctx.sp, ctx.mul
+        nt, nk = sp.shape
+        a, t = sp.on(g.device)
+        gt = g.t().contiguous()                                   # [nt, mul]: coalesced over c
+        gw = torch.empty(nk, mul, device=g.device, dtype=torch.float32)
+        _spmm(t, nk, gt, mul, 1, mul, gw, mul, 1)
+        return gw, None
+
+
+def symcon_coefficients(w: torch.Tensor, sp: SparseRows) -> torch.Tensor:
+    return _SymConCoef.apply(w, sp)

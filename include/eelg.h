@@ -68,6 +68,23 @@ int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
                          const float* row_scale, float scale, int n_rows, int width, float* out,
                          void* stream);
 
+/* Few long segments (per-graph pooling): each segment is cut into n_split pieces summed
+ * separately into work[n_rows, n_split, width], then combined in a fixed order:
+ * out[r, :] = scale * row_scale[r] * sum_pieces.  Same result contract as
+ * eelg_segment_sum_csr (gnn/model.py:100-106 global mean pool), without the
+ * one-wave-per-segment serialisation. */
+int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
+                           const float* row_scale, float scale, int n_rows, int width, int n_split,
+                           float* work, float* out, void* stream);
+
+/* Sparse (CSR) x dense with strided operands:
+ * out[r*ldo_r + c*ldo_c] = sum_{j in row r} val[j] * B[col[j]*ldb_r + c*ldb_c].
+ * Builds the symmetric-contraction coefficients coef = U_sym . W and their weight
+ * gradient U_sym^T . g (U_sym 1.6 % dense; replaces the dense U.W contraction of
+ * gnn/mace.py:242-277 at the weight level). */
+int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_rows, const float* B,
+                  int ldb_r, int ldb_c, int n_cols, float* out, int ldo_r, int ldo_c, void* stream);
+
 /* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
  * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
  * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms]. */

@@ -77,6 +77,42 @@ def test_segment_sum_empty_rows_and_zero_edges():
     assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("sizes", [[1024] * 32, [700, 0, 1, 2049, 64], [5]])
+def test_segment_sum_long_segments(sizes):
+    """graph pooling path (few long segments, split + fixed-order combine); 1e-6."""
+    from gnn import ops
+    ptr = torch.zeros(len(sizes) + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(torch.tensor(sizes), 0).to(torch.int32)
+    n = int(ptr[-1])
+    src = torch.randn(n, 400, dtype=torch.float64)
+    scale = torch.rand(len(sizes), dtype=torch.float64) + 0.5
+    out = ops.segment_sum_long(src.float().to(DEV), ptr.to(DEV), len(sizes),
+                               row_scale=scale.float().to(DEV), scale=2.0)
+    seg = torch.repeat_interleave(torch.arange(len(sizes)), torch.tensor(sizes))
+    ref = 2.0 * scale[:, None] * torch.zeros(len(sizes), 400, dtype=torch.float64).index_add_(0, seg, src)
+    assert rel_err(out, ref) < 1e-6
+
+
+def test_symcon_sparse_coefficients_and_grad():
+    """coef = (U_sym W)^T through the CSR kernel, and its weight gradient, vs dense fp64."""
+    from gnn.mace import SymmetricContraction
+    torch.manual_seed(0)
+    sc = SymmetricContraction("32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+32x1o+32x2e+32x3o+32x4e", 3).to(DEV)
+    coef = sc.coefficients()
+    g = torch.randn_like(coef)
+    (coef * g).sum().backward()
+    u = sc.u_sym.double().cpu()
+    wm = sc.weight_matrix().detach().double().cpu()
+    ref = (u @ wm).t()
+    assert rel_err(coef, ref) < 1e-6
+    gw = u.t() @ g.double().cpu().t()                           # d/dW of sum(coef * g)
+    got = torch.cat([p.grad.reshape(-1) for p in sc.parameters()])
+    wm_params = sc.weight_matrix()                               # same parameter order
+    ws = torch.autograd.grad(wm_params, list(sc.parameters()), gw.to(DEV).float())
+    want = torch.cat([w.reshape(-1) for w in ws])
+    assert rel_err(got, want) < 1e-5
+
+
 def _block_pair(layer_index: int, message_passes: int = 2):
     from gnn.model import EnergyEquivGNN
     p = params(message_passes)
