@@ -99,6 +99,129 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
                       f"{layers} layers, median of {len(times)} step(s) ({med:.2f} s/step)"}
 
 
+def cgc_fwd_bytes(n: int, e: int, d: int) -> int:
+    """Algorithmic bytes of one fused CGC edge-conv launch: node projections ps, pr [N, 2D]
+    and edge projections ep [E, 2D] read once, sender [E] + rowptr [N+1], agg [N, D] written."""
+    return 4 * (2 * n * 2 * d + e * 2 * d + e + (n + 1) + n * d)
+
+
+def cpu_baseline_cgc(modified: bool, p, n_nodes: int, n_edges: int, budget_s: float):
+    """The CGC oracle (oracle/cgc.py, the reference's torch ops on CPU) on one graph of the
+    same shape: fwd + loss + bwd, median over steps within ``budget_s``."""
+    import oracle.cgc as ocgc
+    from gnn.data import collate
+    from gnn.synthetic import SyntheticLattices
+    from gnn.train import stiffness_loss
+    ds = SyntheticLattices(1, n_nodes, n_edges, 1234)
+    b = collate([ds[0]])
+    torch.manual_seed(0)
+    m = (ocgc.CrystGraphConv if modified else ocgc.CrystGraphConvVanilla)(p)
+    iu = torch.triu_indices(6, 6)
+    tgt = b.stiffness if modified else b.stiffness[:, iu[0], iu[1]]
+    times, t_start = [], time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        m.zero_grad(set_to_none=True)
+        stiffness_loss(m(b)["stiffness"], tgt).backward()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s or len(times) >= 50:
+            break
+    med = statistics.median(times)
+    return {"value": round(1.0 / med, 3), "unit": "lattice-graphs/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} "
+                                      f"edges, median of {len(times)} step(s) ({med * 1e3:.1f} ms/step)"}
+
+
+def main_cgc(args):
+    """BASELINE config 4: CGC / mCGC (scripts/train_cgcnn_*.py) on the same synthetic lattices.
+    One step = forward + loss + backward + flat all-reduce + AdamW (hidden 128 / 64, 3 passes)."""
+    from argparse import Namespace
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    from gnn import cgc, ops
+    from gnn.data import collate
+    from gnn.parallel import FlatGradAllReduce, broadcast_parameters
+    from gnn.synthetic import SyntheticLattices
+    from gnn.train import stiffness_loss
+    modified = args.model == "cgc_modified"
+    hid = 128 if modified else 64
+    p = Namespace(hidden_irreps=hid, interaction_reduction="sum", global_reduction="mean",
+                  message_passes=3, positive="square")
+    ds = SyntheticLattices(args.batch * world, args.nodes, args.edges, 1234)
+    batch = collate([ds[rank * args.batch + g] for g in range(args.batch)]).to(dev)
+    torch.manual_seed(0)
+    model = (cgc.CrystGraphConv if modified else cgc.CrystGraphConvVanilla)(p).to(dev)
+    from gnn import EnergyEquivGNN
+    EnergyEquivGNN.edge_graph(batch)
+    iu = torch.triu_indices(6, 6)
+    target = batch.stiffness if modified else batch.stiffness[:, iu[0], iu[1]]
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True, weight_decay=1e-8)
+    broadcast_parameters(model)
+    allreduce = FlatGradAllReduce(list(model.parameters()))
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = stiffness_loss(model(batch)["stiffness"], target)
+        loss.backward()
+        allreduce()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.TIMER.enabled = True
+    ops.TIMER.records.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ksum = ops.TIMER.summary()
+    if rank == 0:
+        n_tot, e_tot = args.batch * args.nodes, args.batch * args.edges
+        roof = None
+        if "cgc_fwd" in ksum:
+            byts = cgc_fwd_bytes(n_tot, e_tot, hid)
+            ms = ksum["cgc_fwd"]["mean_ms"]
+            ach = byts / (ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": "cgc_fwd (fused gather + softplus*sigmoid + segmented sum)",
+                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum["cgc_fwd"]["count"]}
+        out = {"metric": f"lattice-graphs/s (fwd+bwd), {args.model} 3-layer, ~1k nodes/~4k edges",
+               "value": round(world * args.batch * args.steps / dt, 2), "unit": "lattice-graphs/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic periodic lattices (SURVEY 8d generator), random-init weights",
+               "config": {"workload": f"{args.model} hidden {hid}, {args.batch} graphs/GPU x "
+                                      f"{args.nodes} nodes/{args.edges} edges, fwd+loss+bwd+allreduce+AdamW",
+                          "global_batch": args.batch * world, "parallelism": f"graph-sharded dp{world}"},
+               "loss": round(float(loss.item()), 6), "roofline": roof, "cpu_baseline": None}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_cgc(modified, p, args.nodes, args.edges, min(args.cpu_budget, 10.0))
+        if args.kernel_summary:
+            print(json.dumps(ksum, indent=1), file=sys.stderr)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,7 +235,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
+    ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"],
+                    help="egnn = the headline EnergyEquivGNN; cgc_* = BASELINE config 4 benchmark models")
     args = ap.parse_args()
+    if args.model != "egnn":
+        return main_cgc(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

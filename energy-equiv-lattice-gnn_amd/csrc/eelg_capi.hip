@@ -13,6 +13,7 @@
 #include "eelg_internal.h"
 #include "generated/eelg_gen.hip"
 #include "eelg_linear.hip"
+#include "eelg_cgc.hip"
 
 #define EELG_VERSION "eelg 0.1.0 gfx950"
 
@@ -268,6 +269,26 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
   hipLaunchKernelGGL(segment_combine_kernel, dim3((n_rows * width + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, work, row_scale, scale, n_rows, width, n_split, out);
   return check_launch("segment_sum_split");
+}
+
+int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
+                 const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
+                 void* stream) {
+  if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(cgc_fwd_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                     pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
+  return check_launch("cgc_fwd");
+}
+
+int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* sender,
+                 const int* rowptr, const float* row_scale, int n_nodes, int D,
+                 const float* grad_agg, float* dz, float* grad_pr, void* stream) {
+  if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(cgc_bwd_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                     pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
+  return check_launch("cgc_bwd");
 }
 
 int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_rows, const float* B,

@@ -14,9 +14,11 @@ import torch
 
 
 def stiffness_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    """``scripts/train_utils.py:52-60``."""
-    mean_stiffness = target.pow(2).mean(dim=(1, 2))
-    per_graph = torch.nn.functional.mse_loss(pred, target, reduction="none").mean(dim=(1, 2))
+    """``scripts/train_utils.py:52-60`` (per-graph means over every non-batch dim: [B, 6, 6]
+    as the reference, or the 21-vector of the vanilla CGC benchmark)."""
+    dims = tuple(range(1, target.dim()))
+    mean_stiffness = target.pow(2).mean(dim=dims)
+    per_graph = torch.nn.functional.mse_loss(pred, target, reduction="none").mean(dim=dims)
     return 100 * (per_graph / mean_stiffness).mean()
 
 

@@ -77,6 +77,22 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
                            const float* row_scale, float scale, int n_rows, int width, int n_split,
                            float* work, float* out, void* stream);
 
+/* Crystal-graph edge convolution (CGC/mCGC benchmark models): replaces
+ *   c = cat([x[sender], x[receiver], edge_ft]); msg = softplus(fc_values(c)) * sigmoid(fc_multip(c));
+ *   scatter(msg, receiver, reduce)          (scripts/benchmark_models/cgc_modified.py:20-25,
+ *                                            cgc_vanilla.py:20-25, gnn/blocks.py:960-966)
+ * with the linear split by input block: ps = x W_s^T, pr = x W_r^T + b ([N, 2D], values
+ * then multipliers), ep = edge_ft W_e^T ([E, 2D], receiver-sorted edge order).
+ * agg[n] = row_scale[n] * sum_e softplus(zv) sigmoid(zm)  (row_scale NULL -> 'sum'). */
+int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
+                 const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
+                 void* stream);
+/* Backward: dz[E, 2D] = d agg / d z per edge and grad_pr[N, 2D] = receiver sums of dz;
+ * the sender sums are eelg_segment_sum_csr(dz, srowptr, sperm). */
+int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* sender,
+                 const int* rowptr, const float* row_scale, int n_nodes, int D,
+                 const float* grad_agg, float* dz, float* grad_pr, void* stream);
+
 /* Sparse (CSR) x dense with strided operands:
  * out[r*ldo_r + c*ldo_c] = sum_{j in row r} val[j] * B[col[j]*ldb_r + c*ldb_c].
  * Builds the symmetric-contraction coefficients coef = U_sym . W and their weight

@@ -49,11 +49,13 @@ def reshape_irreps(irreps, tensor: torch.Tensor) -> torch.Tensor:
     return torch.cat(out, dim=-1)
 
 
-def get_edge_vectors_and_lengths(positions, edge_index, shifts):
-    """``gnn/mace.py:338-352`` with ``normalize=False``."""
+def get_edge_vectors_and_lengths(positions, edge_index, shifts, normalize=False, eps=1e-9):
+    """``gnn/mace.py:338-352`` (``normalize`` divides by ``length + eps``)."""
     sender, receiver = edge_index
     vectors = positions[receiver] - positions[sender] + shifts
     lengths = torch.linalg.norm(vectors, dim=-1, keepdim=True)
+    if normalize:
+        return vectors / (lengths + eps), lengths
     return vectors, lengths
 
 

@@ -1,0 +1,115 @@
+"""CGC / mCGC benchmark models: oracle checks on CPU, HIP parity
+on the GPU (fp32 HIP vs fp64 oracle; layer 2e-5, model 1e-4 relative to max, grads 1e-3)."""
+from argparse import Namespace
+
+import pytest
+import torch
+
+import oracle.cgc as ocgc
+from helpers import batch, batch_to
+
+F64 = torch.float64
+
+
+def cgc_params(hidden=32, reduction="sum", positive="square", passes=3):
+    return Namespace(hidden_irreps=hidden, interaction_reduction=reduction, global_reduction="mean",
+                     message_passes=passes, positive=positive)
+
+
+def test_oracle_cgc_layer_formula():
+    """msg_e = softplus(W_v c + b_v) * sigmoid(W_m c + b_m), summed at the receiver."""
+    torch.manual_seed(0)
+    layer = ocgc.CGCLayer(4, 4).double()
+    x = torch.randn(3, 4, dtype=F64)
+    ef = torch.randn(2, 4, dtype=F64)
+    ei = torch.tensor([[0, 2], [1, 1]])
+    out = layer(x, ei, ef)
+    manual = torch.zeros(3, 4, dtype=F64)
+    for e in range(2):
+        c = torch.cat([x[ei[0, e]], x[ei[1, e]], ef[e]])
+        v = layer.fc_values.weight @ c + layer.fc_values.bias
+        m = layer.fc_multip.weight @ c + layer.fc_multip.bias
+        manual[ei[1, e]] += torch.log1p(torch.exp(v)) / (1 + torch.exp(-m))
+    assert torch.allclose(out, manual, atol=1e-12)
+
+
+def test_oracle_mcgc_output_symmetric_psd_and_param_count():
+    torch.manual_seed(0)
+    m = ocgc.CrystGraphConv(cgc_params(hidden=128)).double()
+    # reference params (scripts/train_cgcnn_modified.py:26-30): 324,245 weights
+    assert sum(p.numel() for p in m.parameters()) == 324245
+    b, _ = batch(2, 20, 80, 5)
+    c = m(batch_to(b, "cpu", F64))["stiffness"]
+    assert torch.allclose(c, c.transpose(1, 2))
+    assert (torch.linalg.eigvalsh(c) > -1e-10).all()
+
+
+def test_product_cgc_param_names_match_oracle():
+    from gnn.cgc import CrystGraphConv, CrystGraphConvVanilla
+    for pc, oc in ((CrystGraphConv, ocgc.CrystGraphConv), (CrystGraphConvVanilla, ocgc.CrystGraphConvVanilla)):
+        a, o = pc(cgc_params(64)), oc(cgc_params(64))
+        assert {k: v.shape for k, v in a.named_parameters()} == {k: v.shape for k, v in o.named_parameters()}
+
+
+def test_benchmark_models_import_path():
+    from benchmark_models.cgc_modified import CrystGraphConv as A
+    from benchmark_models.cgc_vanilla import CrystGraphConv as B
+    from gnn.cgc import CrystGraphConv, CrystGraphConvVanilla
+    assert A is CrystGraphConv and B is CrystGraphConvVanilla
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reduction,d", [("sum", 128), ("mean", 64), ("sum", 96)])
+def test_cgc_layer_fwd_bwd(reduction, d):
+    from gnn.cgc import CGCLayer
+    torch.manual_seed(1)
+    o = ocgc.CGCLayer(d, d, reduction).double()
+    m = CGCLayer(d, d, reduction).cuda()
+    m.load_state_dict({k: v.float() for k, v in o.state_dict().items()})
+    b, _ = batch(3, 40, 160, 11)
+    ei = b.edge_index
+    n, e = b.node_attrs.shape[0], ei.shape[1]
+    x = torch.randn(n, d, dtype=F64)
+    ef = torch.randn(e, d, dtype=F64)
+    ei[:, 5] = ei[:, 4]                      # a repeated edge
+    xo, eo = x.clone().requires_grad_(True), ef.clone().requires_grad_(True)
+    yo = o(xo, ei, eo)
+    g = torch.randn_like(yo)
+    (yo * g).sum().backward()
+    xm, em = x.float().cuda().requires_grad_(True), ef.float().cuda().requires_grad_(True)
+    ym = m(xm, ei.cuda(), em)
+    (ym * g.float().cuda()).sum().backward()
+    assert _rel(ym, yo) < 2e-5
+    assert _rel(xm.grad, xo.grad) < 2e-5
+    assert _rel(em.grad, eo.grad) < 2e-5
+    po = dict(o.named_parameters())
+    for k, p in m.named_parameters():
+        assert _rel(p.grad, po[k].grad) < 2e-5, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["modified", "vanilla"])
+def test_cgc_model_fwd_bwd_matches_oracle(variant):
+    from gnn import cgc
+    torch.manual_seed(0)
+    p = cgc_params(hidden=128 if variant == "modified" else 64)
+    oc, pc = ((ocgc.CrystGraphConv, cgc.CrystGraphConv) if variant == "modified"
+              else (ocgc.CrystGraphConvVanilla, cgc.CrystGraphConvVanilla))
+    o = oc(p).double()
+    m = pc(p).cuda()
+    m.load_state_dict({k: v.float() for k, v in o.state_dict().items()})
+    b, _ = batch(4, 50, 200, 1234)
+    co = o(batch_to(b, "cpu", F64))["stiffness"]
+    t = torch.randn_like(co)
+    (co * t).sum().backward()
+    cm = m(b.to("cuda"))["stiffness"]
+    (cm * t.float().cuda()).sum().backward()
+    assert _rel(cm, co) < 1e-4
+    po = dict(o.named_parameters())
+    for k, q in m.named_parameters():
+        assert _rel(q.grad, po[k].grad) < 1e-3, k
