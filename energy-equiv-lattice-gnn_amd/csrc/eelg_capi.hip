@@ -202,6 +202,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
+  info[5] = c.Dout;
   *sig = c.sig;
   return 0;
 }
@@ -328,11 +329,13 @@ int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_
   return check_launch("sc_bwd_x");
 }
 
-int eelg_sc_cmajor(int cfg, const float* x, int n_nodes, int mul, float* xt, void* stream) {
+int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
+                   void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
+  if (which != 0 && which != 1) return fail(-2, "sc_cmajor: which must be 0 (input) or 1 (output)");
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->cmajor, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(which ? c->cmajor_out : c->cmajor, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, x, n_nodes, xt);
   return check_launch("sc_cmajor");
 }

@@ -22,12 +22,13 @@ struct eelg_tp_cfg {
 
 struct eelg_sc_cfg {
   const char* name;
-  int D, drow, orow, nterms, njg;
+  int D, Dout, drow, orow, nterms, njg;
   uint64_t sig;
   eelg_sc_fwd_fn fwd;
   eelg_sc_bwdx_fn bwd_x;
   eelg_sc_bwdc_fn bwd_coef;
-  eelg_sc_cmajor_fn cmajor;
+  eelg_sc_cmajor_fn cmajor;      // input (coupling) layout
+  eelg_sc_cmajor_fn cmajor_out;  // output layout
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -63,10 +63,15 @@ def tp_configs() -> Dict[str, Tuple[Irreps, Irreps, Irreps]]:
 
 
 def sc_configs() -> Dict[str, Tuple[str, Tuple[int, ...], int]]:
+    """coupling = the interaction irreps (SH lmax), outputs = the hidden irreps.  Hidden
+    irreps beyond the SH lmax are not generated: the reference's U_matrix_real fails for
+    them (an output irrep with no degree-1 path leaves ``last_ir`` unbound,
+    gnn/mace.py:466-476)."""
     out = {}
-    for lmax in (3, 4):
+    for lmax, hmax in ((3, 3), (4, 4)):
         coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
-        out[f"sc_l{lmax}_c3"] = (coupling, tuple(range(lmax + 1)), 3)
+        key = f"sc_l{lmax}_c3" if hmax == lmax else f"sc_l{lmax}h{hmax}_c3"
+        out[key] = (coupling, tuple(range(hmax + 1)), 3)
     return out
 
 
@@ -362,68 +367,79 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     of 4 waves owns 4 consecutive channels ("channel quad") x 64 nodes and stages
     the quad's 4*D floats per node through LDS with contiguous global segments, so
     every byte of x / out crosses HBM once.  One wave = one channel (wave-uniform,
-    coefficients come through scalar loads), one lane = one node."""
+    coefficients come through scalar loads), one lane = one node.  The output irreps
+    (``ls``, parity (-1)^l) may differ from the coupling irreps of the input (the
+    reference's product block maps the interaction irreps onto the hidden irreps)."""
     plan = cg.symcon_plan(coupling, ls, corr)
     irs = [ir for _, ir in Irreps(coupling)]
-    assert tuple(ir.l for ir in irs) == tuple(ls), "in/out irreps must match"
-    D = sum(ir.dim for ir in irs)
+    out_irs = [Ir(l, (-1) ** l) for l in ls]
     Q = 4                                   # channels per workgroup
-    QD = Q * D                              # floats per node in a quad tile
-    TP = QD + 1                             # padded LDS row (odd -> conflict-free)
-    comp = []                               # component a -> (l, m, row offset of block, seg start)
-    off = seg = 0
-    for ir in irs:
-        for m in range(ir.dim):
-            comp.append((ir.l, m, off, seg))
-        off += MUL * ir.dim
-        seg += Q * ir.dim
-    drow = off
+
+    class Lay:
+        """per-channel component list of one row layout"""
+        def __init__(self, irreps, tag):
+            self.comp, off, seg = [], 0, 0   # component a -> (l, m, row offset, seg start)
+            self.segs = []
+            for ir in irreps:
+                for m in range(ir.dim):
+                    self.comp.append((ir.l, m, off, seg))
+                self.segs.append((seg, seg + Q * ir.dim, off, ir.dim))
+                off += MUL * ir.dim
+                seg += Q * ir.dim
+            self.D = len(self.comp)
+            self.QD = Q * self.D
+            self.row = off
+            self.goff = f"sc_goff_{name}_{tag}"
+
+    lin, lout = Lay(irs, "in"), Lay(out_irs, "out")
+    D, Dout = lin.D, lout.D
+    TP = max(lin.QD, lout.QD) + 1           # padded LDS row shared by in / out tiles
+    if TP % 2 == 0:
+        TP += 1                             # odd -> conflict-free lane rows
+    drow, orow = lin.row, lout.row
     nt = len(plan.terms)
 
-    def lq(a, cl):
+    def lq(lay, a, cl):
         """LDS column of component a for channel-in-quad cl (may be a runtime expr)."""
-        l, m, _, sg = comp[a]
+        l, m, _, sg = lay.comp[a]
         return f"{sg} + ({cl}) * {2 * l + 1} + {m}"
 
     L: List[str] = []
-    L.append(f"// ===== symmetric contraction config {name}: coupling {coupling}, correlation {corr} =====")
-    L.append(f"// {nt} polynomial terms per channel; rows of {drow} floats; quad tile {QD} floats/node")
+    L.append(f"// ===== symmetric contraction config {name}: coupling {coupling} -> ls {ls}, correlation {corr} =====")
+    L.append(f"// {nt} polynomial terms per channel; rows of {drow} -> {orow} floats")
 
-    # global offset of quad-tile column q for channel quad cq
-    L.append(f"__device__ __forceinline__ int sc_goff_{name}(int q, int cq) {{")
-    segs = []
-    o2 = s2 = 0
-    for ir in irs:
-        segs.append((s2, s2 + Q * ir.dim, o2, ir.dim))
-        o2 += MUL * ir.dim
-        s2 += Q * ir.dim
-    for (a, b, o, d) in segs[:-1]:
-        L.append(f"  if (q < {b}) return {o} + cq * {Q * d} + (q - {a});")
-    a, b, o, d = segs[-1]
-    L.append(f"  return {o} + cq * {Q * d} + (q - {a});")
-    L.append("}")
+    # global offset of quad-tile column q for channel quad cq (per layout)
+    for lay in ((lin,) if lout.comp == lin.comp else (lin, lout)):
+        L.append(f"__device__ __forceinline__ int {lay.goff}(int q, int cq) {{")
+        for (a, b, o, d) in lay.segs[:-1]:
+            L.append(f"  if (q < {b}) return {o} + cq * {Q * d} + (q - {a});")
+        a, b, o, d = lay.segs[-1]
+        L.append(f"  return {o} + cq * {Q * d} + (q - {a});")
+        L.append("}")
+    if lout.comp == lin.comp:
+        lout.goff = lin.goff
 
-    def stage_in(src, tile):
-        per = (64 * QD + 255) // 256
+    def stage_in(src, tile, lay):
+        per = (64 * lay.QD + 255) // 256
         out = ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                "#pragma unroll 2",
                f"  for (int it = 0; it < {per}; ++it) {{",
                f"    const int idx = tid + 256 * it;",
-               f"    if (idx < {64 * QD}) {{",
-               f"      const int nl = idx / {QD}, q = idx - nl * {QD}, n = n0 + nl;",
-               f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {drow} + sc_goff_{name}(q, cq)] : 0.0f;",
+               f"    if (idx < {64 * lay.QD}) {{",
+               f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
+               f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] : 0.0f;",
                "    }", "  } }"]
         return out
 
-    def stage_out(dst, tile):
-        per = (64 * QD + 255) // 256
+    def stage_out(dst, tile, lay):
+        per = (64 * lay.QD + 255) // 256
         return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                 "#pragma unroll 2",
                 f"  for (int it = 0; it < {per}; ++it) {{",
                 f"    const int idx = tid + 256 * it;",
-                f"    if (idx < {64 * QD}) {{",
-                f"      const int nl = idx / {QD}, q = idx - nl * {QD}, n = n0 + nl;",
-                f"      if (n < n_nodes) {dst}[(size_t)n * {drow} + sc_goff_{name}(q, cq)] = {tile}[nl * {TP} + q];",
+                f"    if (idx < {64 * lay.QD}) {{",
+                f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
+                f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = {tile}[nl * {TP} + q];",
                 "    }", "  } }"]
 
     # group terms by (a, b) pair
@@ -451,16 +467,15 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[64 * {TP}];")
     L += head
-    L += stage_in("x", "tile")
+    L += stage_in("x", "tile", lin)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = tr[{lq(a, 'cl')}];")
-    for q in range(D):
+        L.append(f"  float x{a} = tr[{lq(lin, a, 'cl')}];")
+    for q in range(Dout):
         L.append(f"  float o{q} = 0.0f;")
-    fpin = pin([f"x{a}" for a in range(D)] + [f"o{q}" for q in range(D)])
     blocks = sc_blocks(plan)
-    fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(D)]
+    fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
     for t in blocks[0]["terms"]:
         L.append(f"  float c{t} = cf[{t}];")
     for bi, blk in enumerate(blocks):
@@ -487,10 +502,10 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 carry = [pv]
         L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
-    for q in range(D):
-        L.append(f"  tr[{lq(q, 'cl')}] = o{q};")
+    for q in range(Dout):
+        L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
     L.append("  __syncthreads();")
-    L += stage_out("out", "tile")
+    L += stage_out("out", "tile", lout)
     L.append("}")
 
     # ---------------- backward w.r.t. x ----------------
@@ -500,18 +515,17 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  __shared__ float tx[64 * {TP}];")
     L.append(f"  __shared__ float tg[64 * {TP}];")
     L += head
-    L += stage_in("x", "tx")
-    L += stage_in("gout", "tg")
+    L += stage_in("x", "tx", lin)
+    L += stage_in("gout", "tg", lout)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
     L.append(f"  const float* __restrict__ gr = tg + lane * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = xr[{lq(a, 'cl')}];")
+        L.append(f"  float x{a} = xr[{lq(lin, a, 'cl')}];")
         L.append(f"  float d{a} = 0.0f;")
-    for q in range(D):
-        L.append(f"  float g{q} = gr[{lq(q, 'cl')}];")
-    bpin = pin([f"x{a}" for a in range(D)] + [f"g{q}" for q in range(D)] + [f"d{a}" for a in range(D)])
-    bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(D)] + [f"d{a}" for a in range(D)]
+    for q in range(Dout):
+        L.append(f"  float g{q} = gr[{lq(lout, q, 'cl')}];")
+    bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     for t in blocks[0]["terms"]:
         L.append(f"  float c{t} = cf[{t}];")
     for bi, blk in enumerate(blocks):
@@ -541,35 +555,43 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for a in range(D):
-        L.append(f"  xr[{lq(a, 'cl')}] = d{a};")
+        L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
     L.append("  __syncthreads();")
-    L += stage_out("gx", "tx")
+    L += stage_out("gx", "tx", lin)
     L.append("}")
 
     # ---------------- mul-major -> channel-major transpose ----------------
-    # dst[(c * D + a) * n_nodes + n] = src[n, a-th component of channel c]
-    L.append(f"__global__ __launch_bounds__(256) void sc_cmajor_{name}(")
-    L.append("    const float* __restrict__ x, int n_nodes, float* __restrict__ xt) {")
-    L.append(f"  __shared__ float tile[64 * {TP}];")
-    L.append("  const int cq = blockIdx.x;")
-    L.append("  const int n0 = blockIdx.y * 64;")
-    L += stage_in("x", "tile")
-    L.append("  __syncthreads();")
-    sgs = ", ".join(str(comp[a][3]) for a in range(D))
-    dls = ", ".join(str(2 * comp[a][0] + 1) for a in range(D))
-    ms = ", ".join(str(comp[a][1]) for a in range(D))
-    L.append(f"  const int kseg[{D}] = {{{sgs}}}, kd[{D}] = {{{dls}}}, km[{D}] = {{{ms}}};")
-    per = (Q * D * 64 + 255) // 256
-    L.append(f"  for (int it = 0; it < {per}; ++it) {{")
-    L.append("    const int idx = threadIdx.x + 256 * it;")
-    L.append(f"    if (idx < {Q * D * 64}) {{")
-    L.append("      const int row = idx >> 6, nl = idx & 63, n = n0 + nl;")
-    L.append(f"      const int cl = row / {D}, a = row - cl * {D};")
-    L.append(f"      if (n < n_nodes) xt[(size_t)((cq * {Q} + cl) * {D} + a) * n_nodes + n] = "
-             f"tile[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];")
-    L.append("    }")
-    L.append("  }")
-    L.append("}")
+    # dst[(c * D + a) * n_nodes + n] = src[n, a-th component of channel c]; one kernel per
+    # distinct layout (x uses the input layout, grad_out the output layout)
+    def emit_cmajor(kname, lay):
+        L.append(f"__global__ __launch_bounds__(256) void {kname}(")
+        L.append("    const float* __restrict__ x, int n_nodes, float* __restrict__ xt) {")
+        L.append(f"  __shared__ float tile[64 * {TP}];")
+        L.append("  const int cq = blockIdx.x;")
+        L.append("  const int n0 = blockIdx.y * 64;")
+        L.extend(stage_in("x", "tile", lay))
+        L.append("  __syncthreads();")
+        dd = lay.D
+        sgs = ", ".join(str(lay.comp[a][3]) for a in range(dd))
+        dls = ", ".join(str(2 * lay.comp[a][0] + 1) for a in range(dd))
+        ms = ", ".join(str(lay.comp[a][1]) for a in range(dd))
+        L.append(f"  const int kseg[{dd}] = {{{sgs}}}, kd[{dd}] = {{{dls}}}, km[{dd}] = {{{ms}}};")
+        per = (Q * dd * 64 + 255) // 256
+        L.append(f"  for (int it = 0; it < {per}; ++it) {{")
+        L.append("    const int idx = threadIdx.x + 256 * it;")
+        L.append(f"    if (idx < {Q * dd * 64}) {{")
+        L.append("      const int row = idx >> 6, nl = idx & 63, n = n0 + nl;")
+        L.append(f"      const int cl = row / {dd}, a = row - cl * {dd};")
+        L.append(f"      if (n < n_nodes) xt[(size_t)((cq * {Q} + cl) * {dd} + a) * n_nodes + n] = "
+                 f"tile[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];")
+        L.append("    }")
+        L.append("  }")
+        L.append("}")
+    emit_cmajor(f"sc_cmajor_{name}", lin)
+    cmajor_out = f"sc_cmajor_{name}"
+    if lout.comp != lin.comp:
+        cmajor_out = f"sc_cmajor_out_{name}"
+        emit_cmajor(cmajor_out, lout)
 
     # ---------------- backward w.r.t. coefficients ----------------
     JG = 64
@@ -582,12 +604,12 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
     L.append(f"  __shared__ float sx[{D} * 64];")
-    L.append(f"  __shared__ float sg[{D} * 64];")
+    L.append(f"  __shared__ float sg[{Dout} * 64];")
     L.append("  const int c = blockIdx.z;")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
     L.append(f"  const int jg = __builtin_amdgcn_readfirstlane(blockIdx.x * {WPB} + wv);")
     L.append(f"  const float* __restrict__ xs = xt + (size_t)c * {D} * n_nodes;")
-    L.append(f"  const float* __restrict__ gs = gt + (size_t)c * {D} * n_nodes;")
+    L.append(f"  const float* __restrict__ gs = gt + (size_t)c * {Dout} * n_nodes;")
     L.append("  const int nb = blockIdx.y * chunk;")
     L.append("  const int ne = min(n_nodes, nb + chunk);")
     L.append(f"  float acc[{JG}];")
@@ -595,7 +617,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = 0.0f;")
     # double-buffered staging: the next tile's global loads are in flight (in
     # registers) while the current tile is consumed from LDS
-    per = (D * 64 + 64 * WPB - 1) // (64 * WPB)
+    per = (max(D, Dout) * 64 + 64 * WPB - 1) // (64 * WPB)
     for it in range(per):
         L.append(f"  float rx{it} = 0.0f, rg{it} = 0.0f;")
 
@@ -603,8 +625,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         out = []
         for it in range(per):
             out.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; const int a = idx >> 6, n = {base} + (idx & 63);")
-            out.append(f"      if (idx < {D * 64} && n < ne) {{ rx{it} = xs[(size_t)a * n_nodes + n]; rg{it} = gs[(size_t)a * n_nodes + n]; }}"
-                       f" else {{ rx{it} = 0.0f; rg{it} = 0.0f; }} }}")
+            out.append(f"      rx{it} = (idx < {D * 64} && n < ne) ? xs[(size_t)a * n_nodes + n] : 0.0f;"
+                       f" rg{it} = (idx < {Dout * 64} && n < ne) ? gs[(size_t)a * n_nodes + n] : 0.0f; }}")
         return out
     L += issue("nb")
 
@@ -612,7 +634,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         """the 64-node tile loop; every wave of the workgroup runs it (same barrier count)"""
         out = ["      for (int n0 = nb; n0 < ne; n0 += 64) {"]
         for it in range(per):
-            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) {{ sx[idx] = rx{it}; sg[idx] = rg{it}; }} }}")
+            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) sx[idx] = rx{it};"
+                       f" if (idx < {Dout * 64}) sg[idx] = rg{it}; }}")
         out.append("        __syncthreads();")
         out.append("        if (n0 + 64 < ne) {")
         out += ["    " + ln for ln in issue("n0 + 64")]
@@ -689,8 +712,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"    {{ const int t = jg * {JG} + {R} * lane + {i}; if (t < {nt}) dst[t] = acc[{i}]; }}")
     L.append("  }")
     L.append("}")
-    info = dict(D=D, drow=drow, orow=drow, nterms=nt, njg=len(groups), wpb=WPB,
-                sig=fnv1a64(sc_signature(coupling, ls, corr)))
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB,
+                cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
 
@@ -720,8 +743,9 @@ def main(outdir: str) -> None:
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:
-        parts.append(f'  {{"{name}", {i["D"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, '
-                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}}},')
+        parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, '
+                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
+                     f'{i["cmajor_out"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -36,7 +36,7 @@ _SIGS = {
     "eelg_sc_fwd": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
-    "eelg_sc_cmajor": ([_I, _P, _I, _I, _P, _P], _I),
+    "eelg_sc_cmajor": ([_I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
 }
@@ -126,8 +126,46 @@ def sc_config(name: str) -> Tuple[int, Dict[str, int], int]:
     idx = lib.eelg_sc_find(name.encode())
     if idx < 0:
         check(idx, f"sc config {name}")
-    info = (ctypes.c_int * 5)()
+    return (idx,) + _sc_info(idx)
+
+
+def _tp_info(idx: int):
+    info = (ctypes.c_int * 7)()
     sig = ctypes.c_uint64()
-    check(lib.eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P)), "sc_info")
-    keys = ("D", "x_row", "out_row", "nterms", "njg")
-    return idx, dict(zip(keys, list(info))), sig.value
+    rc = load().eelg_tp_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P))
+    if rc != 0:
+        return None
+    keys = ("din", "dmid", "wn", "nsh", "ngroups", "npaths", "lmax")
+    return dict(zip(keys, list(info))), sig.value
+
+
+def _sc_info(idx: int):
+    info = (ctypes.c_int * 6)()
+    sig = ctypes.c_uint64()
+    rc = load().eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P))
+    if rc != 0:
+        return None
+    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout")
+    return dict(zip(keys, list(info))), sig.value
+
+
+def _by_sig(getter, sig: int, what: str):
+    idx = 0
+    while True:
+        got = getter(idx)
+        if got is None:
+            raise EELGError(f"libeelg.so has no generated {what} kernel with structure signature "
+                            f"0x{sig:016x}; add the irreps to csrc/gen_kernels.py and rebuild")
+        if got[1] == sig:
+            return idx, got[0]
+        idx += 1
+
+
+def tp_config_by_sig(sig: int) -> Tuple[int, Dict[str, int]]:
+    """The generated tensor-product kernel set whose structure hash is ``sig``."""
+    return _by_sig(_tp_info, sig, "tensor-product")
+
+
+def sc_config_by_sig(sig: int) -> Tuple[int, Dict[str, int]]:
+    """The generated symmetric-contraction kernel set whose structure hash is ``sig``."""
+    return _by_sig(_sc_info, sig, "symmetric-contraction")

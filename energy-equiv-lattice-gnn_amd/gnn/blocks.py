@@ -160,16 +160,7 @@ class TensorProductInteractionBlock(torch.nn.Module):
         self.conv_tp_weights.append(layer)
         self.irreps_mid = irreps_mid.simplify()
         self.linear = Linear(self.irreps_mid, self._irreps_out, biases=bias)
-        # which generated kernel set serves this block
-        lmax = self.edge_attrs_irreps.lmax
-        hidden = Irreps("+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
-        if self._node_feats_irreps == Irreps("32x0e"):
-            self.cfg_name = f"tpA_l{lmax}"
-        elif self._node_feats_irreps == hidden:
-            self.cfg_name = f"tpB_l{lmax}"
-        else:
-            raise NotImplementedError(f"no generated tensor-product kernel for node irreps "
-                                      f"{self._node_feats_irreps} with SH lmax {lmax}")
+        # the generated kernel set serving this block is found by its structure hash
         self._sig = cg.fnv1a64(cg.tp_signature(self._node_feats_irreps, self.edge_attrs_irreps,
                                                self._irreps_out))
         self._cfg = None
@@ -184,11 +175,7 @@ class TensorProductInteractionBlock(torch.nn.Module):
 
     def _config(self):
         if self._cfg is None:
-            idx, info, sig = _lib.tp_config(self.cfg_name)
-            if sig != self._sig:
-                raise _lib.EELGError(f"libeelg.so was built for a different {self.cfg_name} "
-                                     "structure; rebuild it")
-            self._cfg = (idx, info)
+            self._cfg = _lib.tp_config_by_sig(self._sig)
         return self._cfg
 
     def forward(self, node_feats, edge_attrs, edge_feats, edge_index: EdgeIndex,

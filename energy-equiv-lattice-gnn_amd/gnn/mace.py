@@ -46,12 +46,17 @@ class SymmetricContraction(torch.nn.Module):
         lmax = self.irreps_in.lmax
         ls = tuple(ir.l for _, ir in self.irreps_out)
         expect = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
-        if (coupling != expect or ls != tuple(range(lmax + 1)) or correlation != 3
-                or any(m != self.mul for m, _ in self.irreps_in) or self.mul != 32):
+        if (coupling != expect or correlation != 3 or self.mul != 32
+                or any(m != self.mul for m, _ in self.irreps_in)
+                or any(m != self.mul or ir.p != (-1) ** ir.l for m, ir in self.irreps_out)):
             raise NotImplementedError(
-                f"symmetric contraction kernels are generated for 32x(0e..{lmax}) in/out, "
-                f"correlation 3; got {self.irreps_in} -> {self.irreps_out}, correlation {correlation}")
-        self.cfg_name = f"sc_l{lmax}_c{correlation}"
+                f"symmetric contraction kernels are generated for 32x(0e..{lmax}) inputs, 32x "
+                f"natural-parity outputs, correlation 3; got {self.irreps_in} -> {self.irreps_out}, "
+                f"correlation {correlation}")
+        if any(ir.l > lmax for _, ir in self.irreps_out):
+            raise NotImplementedError(
+                f"output irreps {self.irreps_out} beyond the coupling lmax {lmax}: the reference "
+                "U_matrix_real has no degree-1 path for them (gnn/mace.py:466-476)")
         plan = cg.symcon_plan(coupling, ls, correlation)
         self._sig = cg.fnv1a64(cg.sc_signature(coupling, ls, correlation))
         self.block_order = [(l, nu) for l, nu, _ in plan.weight_blocks]
@@ -66,11 +71,7 @@ class SymmetricContraction(torch.nn.Module):
 
     def _config(self):
         if self._cfg is None:
-            idx, info, sig = _lib.sc_config(self.cfg_name)
-            if sig != self._sig:
-                raise _lib.EELGError(f"libeelg.so was built for a different {self.cfg_name} "
-                                     "structure; rebuild it")
-            self._cfg = (idx, info)
+            self._cfg = _lib.sc_config_by_sig(self._sig)
         return self._cfg
 
     def weight_matrix(self) -> torch.Tensor:

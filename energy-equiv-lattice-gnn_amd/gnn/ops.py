@@ -265,11 +265,11 @@ class _SymCon(torch.autograd.Function):
             TIMER.stop(tok)
         if ctx.needs_input_grad[1]:
             xt = torch.empty(ctx.mul * ctx.info["D"], n, device=x.device, dtype=torch.float32)
-            gt = torch.empty_like(xt)
+            gt = torch.empty(ctx.mul * ctx.info["Dout"], n, device=x.device, dtype=torch.float32)
             tok = TIMER.start("sc_cmajor")
-            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
+            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
                                           _lib.stream()), "sc_cmajor")
-            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
+            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
                                           _lib.stream()), "sc_cmajor")
             TIMER.stop(tok)
             chunk = max(64, min(4096, (n // 16 + 63) // 64 * 64))

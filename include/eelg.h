@@ -35,9 +35,11 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups} */
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out} (D: coupling components
+ * per channel of the input, D_out: of the output; they differ when the product maps the
+ * SH-lmax interaction irreps onto wider hidden irreps) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info5, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info6, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -108,8 +110,10 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
                   int mul, float* grad_x, void* stream);
-/* Channel-major copy xt[(c*D + a)*N + n] of a mul-major row tensor (feeds sc_bwd_coef). */
-int eelg_sc_cmajor(int cfg, const float* x, int n_nodes, int mul, float* xt, void* stream);
+/* Channel-major copy xt[(c*D + a)*N + n] of a mul-major row tensor (feeds sc_bwd_coef);
+ * which = 0: input (coupling) layout, 1: output layout. */
+int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
+                   void* stream);
 /* Coefficient gradient from channel-major x and grad_out:
  * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk) (chunk % 64 == 0);
  * the caller sums over chunks (deterministic). */

@@ -170,12 +170,13 @@ def test_product_block_fwd_bwd():
         assert rel_err(pm.grad, po[name].grad) < 5e-5, name
 
 
-@pytest.mark.parametrize("message_passes", [2, 4])
-def test_model_forward_backward_matches_oracle(message_passes):
+@pytest.mark.parametrize("message_passes,lmax", [(2, 4), (4, 4), (2, 3)])
+def test_model_forward_backward_matches_oracle(message_passes, lmax):
+    """lmax 3 = BASELINE config 5's irreps (SH and hidden irreps up to l = 3)."""
     from gnn.model import EnergyEquivGNN
     from gnn.train import stiffness_loss
     b, bd, csr, rmax = _setup()
-    p = params(message_passes, max_edge_radius=rmax)
+    p = params(message_passes, lmax=lmax, max_edge_radius=rmax)
     torch.manual_seed(0)
     o = omodel.EnergyEquivGNN(p).double()
     m = EnergyEquivGNN(p).to(DEV)

@@ -204,3 +204,11 @@ def test_wgrad_split_k_matches_matmul():
     g = torch.randn(1300, 8, dtype=torch.float64)
     x = torch.randn(1300, 5, dtype=torch.float64)
     assert torch.allclose(_wgrad(g, x, chunk=256), g.t() @ x, atol=1e-10)
+
+
+def test_lmax3_with_l4_hidden_irreps_raises_like_the_reference():
+    """The reference cannot build a product block whose outputs exceed the SH lmax
+    (gnn/mace.py:466-476); the product says so instead of failing inside numpy."""
+    from gnn.mace import SymmetricContraction
+    with pytest.raises(NotImplementedError):
+        SymmetricContraction("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o+32x4e", 3)

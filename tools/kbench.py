@@ -129,11 +129,11 @@ def main():
     gt = torch.empty(800, n, device=dev)
 
     def cm():
-        ops._lib.check(lib.eelg_sc_cmajor(sidx, ops._lib.ptr(xs), n, 32, ops._lib.ptr(xt),
+        ops._lib.check(lib.eelg_sc_cmajor(sidx, 0, ops._lib.ptr(xs), n, 32, ops._lib.ptr(xt),
                                           ops._lib.stream()), "cm")
     rec("sc_cmajor", timeit_if("sc_cmajor", cm, args.reps), 4 * 2 * n * 800)
     cm()
-    ops._lib.check(lib.eelg_sc_cmajor(sidx, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream()), "cm")
+    ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream()), "cm")
     chunk = max(64, min(4096, (n // 16 + 63) // 64 * 64))
     nch = (n + chunk - 1) // chunk
     part = torch.empty(nch, 32, nt, device=dev)
