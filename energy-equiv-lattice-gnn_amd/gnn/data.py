@@ -70,8 +70,11 @@ class Batch(Data):
             elif k in _NODE_KEYS or k in _EDGE_KEYS:
                 b[k] = torch.cat(vals, dim=0)
             elif k in _GRAPH_KEYS and torch.is_tensor(vals[0]):
-                b[k] = torch.cat([v.reshape(1, *v.shape[-2:]) if v.dim() >= 2 else v.reshape(1)
-                                  for v in vals], dim=0)
+                # per-graph targets: [1, 6, 6] / [1, 3, 3, 3, 3] / [6, 6] / scalar -> stacked
+                b[k] = torch.cat([v if (v.dim() >= 3 and v.shape[0] == 1) else
+                                  (v.unsqueeze(0) if v.dim() >= 1 else v.reshape(1)) for v in vals], dim=0)
+            elif isinstance(vals[0], (int, float)) and not isinstance(vals[0], bool):
+                b[k] = torch.tensor(vals)                   # PyG turns numbers into a [B] tensor
             elif torch.is_tensor(vals[0]):
                 b[k] = torch.cat([v.reshape(1, *v.shape) for v in vals], dim=0)
             else:
