@@ -272,15 +272,26 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         for l2 in l2s:
             for j in range(2 * l2 + 1):
                 L.append(f"    float y{l2 * l2 + j} = ye[{l2 * l2 + j}];")
-        bpin_ = pin([f"x{l}_{i}" for i in range(d)] + [f"gx{l}_{i}" for i in range(d)]
+        base_pin = ([f"x{l}_{i}" for i in range(d)] + [f"gx{l}_{i}" for i in range(d)]
                     + [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)])
-        for p in grp:
+
+        def pref(p):
+            """issue the loads one path needs (its grad_agg slot row and weight)"""
+            d3 = 2 * p.l3 + 1
+            out = [f"    float g{p.slot}_{k} = ge[{p.out_off} + u * {d3} + {k}];" for k in range(d3)]
+            out.append(f"    float w{p.slot} = we[{p.slot * MUL}];")
+            return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
+        first, _ = pref(grp[0])
+        L += first
+        for pi, p in enumerate(grp):
             d3 = 2 * p.l3 + 1
             d1 = 2 * p.l1 + 1
+            nxt_regs = []
+            if pi + 1 < len(grp):            # next path's loads in flight during this one
+                code, nxt_regs = pref(grp[pi + 1])
+                L += code
             L.append(f"    {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
             L.append(f"      const float cp = {flit(p.coef)} * inv_norm;")
-            for k in range(d3):
-                L.append(f"      const float g{k} = ge[{p.out_off} + u * {d3} + {k}];")
             nz = _path_cg(p)
             byik: Dict[Tuple[int, int], List[str]] = {}
             for (i, j, k), c in nz:
@@ -291,15 +302,15 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
             for k in range(d3):
                 ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
                 if ts:
-                    gterms.append(f"g{k} * ({' + '.join(ts)})")
+                    gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
             L.append(f"      gwe[{p.slot * MUL}] = cp * ({' + '.join(gterms) if gterms else '0.0f'});")
-            L.append(f"      const float hw = cp * we[{p.slot * MUL}];")
+            L.append(f"      const float hw = cp * w{p.slot};")
             for i in range(d1):
-                ts = [f"m{i}_{k} * g{k}" for k in range(d3) if (i, k) in byik]
+                ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
                 if ts:
                     L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
             L.append("    }")
-            L.append("    " + bpin_)
+            L.append("    " + pin(base_pin + nxt_regs))
         for i in range(d):
             L.append(f"    gxo[{node_off[l]} + u * {d} + {i}] = gx{l}_{i};")
         L.append("    break; }")
@@ -512,19 +523,21 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx) {")
+    # one LDS tile, used three times (x in, grad_out in, grad_x out): 2x the occupancy of
+    # separate x / grad_out tiles
     L.append(f"  __shared__ float tx[64 * {TP}];")
-    L.append(f"  __shared__ float tg[64 * {TP}];")
     L += head
     L += stage_in("x", "tx", lin)
-    L += stage_in("gout", "tg", lout)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
-    L.append(f"  const float* __restrict__ gr = tg + lane * {TP};")
     for a in range(D):
         L.append(f"  float x{a} = xr[{lq(lin, a, 'cl')}];")
         L.append(f"  float d{a} = 0.0f;")
+    L.append("  __syncthreads();")
+    L += stage_in("gout", "tx", lout)
+    L.append("  __syncthreads();")
     for q in range(Dout):
-        L.append(f"  float g{q} = gr[{lq(lout, q, 'cl')}];")
+        L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     for t in blocks[0]["terms"]:
         L.append(f"  float c{t} = cf[{t}];")
