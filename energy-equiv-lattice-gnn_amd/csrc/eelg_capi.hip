@@ -347,7 +347,7 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
   if (chunk <= 0 || chunk % 64) return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of 64");
   if (n_nodes <= 0) return 0;
   const int nch = (n_nodes + chunk - 1) / chunk;
-  hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + 7) / 8, nch, mul), dim3(512), 0,
+  hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + c->wpb - 1) / c->wpb, nch, mul), dim3(64 * c->wpb), 0,
                      (hipStream_t)stream, xt, gt, n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
 }

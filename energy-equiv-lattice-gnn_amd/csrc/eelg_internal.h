@@ -22,7 +22,7 @@ struct eelg_tp_cfg {
 
 struct eelg_sc_cfg {
   const char* name;
-  int D, Dout, drow, orow, nterms, njg;
+  int D, Dout, drow, orow, nterms, njg, wpb;  // wpb: waves (term groups) per coef-grad workgroup
   uint64_t sig;
   eelg_sc_fwd_fn fwd;
   eelg_sc_bwdx_fn bwd_x;

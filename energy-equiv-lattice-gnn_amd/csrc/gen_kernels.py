@@ -608,7 +608,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 
     # ---------------- backward w.r.t. coefficients ----------------
     JG = 64
-    WPB = 8
+    WPB = 8                                   # waves (term groups) per workgroup
     groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
     L.append(f"// coefficient gradient from channel-major x / g: {len(groups)} term groups of <= {JG};")
     L.append(f"// a workgroup = one channel x {WPB} term groups (waves) sharing staged 64-node tiles;")
@@ -756,7 +756,7 @@ def main(outdir: str) -> None:
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:
-        parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, '
+        parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
                      f'{i["cmajor_out"]}}},')
     parts.append("};")
