@@ -203,12 +203,42 @@ __global__ __launch_bounds__(256) void lin_fwd_kernel(const float* __restrict__ 
     const int jw = min(32, sl.n_out - jt * 32);
     const int olen = jw * d;  // floats per node in this column tile
     float* __restrict__ yb = y + (size_t)n_lo * y_row + sl.y_off + (size_t)jt * 32 * d;
-    Walk3 ow;
-    ow.init(tid, 256, jw, d);
-    for (int f = tid; f < span * olen; f += 256) {
-      const int row = (n_lo + ow.a) * d + ow.m - r0;
-      if (row >= 0 && row < LIN_ROWS) yb[(size_t)ow.a * y_row + ow.b * d + ow.m] = Os[row * LIN_ST + ow.b];
-      ow.next(jw, d);
+    const bool vst = (y_row & 3) == 0 && (olen & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                     ((sl.y_off + jt * 32 * d) & 3) == 0;
+    if (vst) {
+      // float4 per-node runs; nodes cut by the workgroup's row range go element-wise
+      Walk3 ow;
+      ow.init(4 * tid, 4 * 256, jw, d);
+      for (int f = 4 * tid; f < span * olen; f += 4 * 256) {
+        const int nrow0 = (n_lo + ow.a) * d - r0;   // row of (node, m = 0)
+        float* dst = yb + (size_t)ow.a * y_row + ow.b * d + ow.m;
+        int jj = ow.b, m = ow.m;
+        if (nrow0 >= 0 && nrow0 + d <= LIN_ROWS) {
+          float v[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            v[t] = Os[(nrow0 + m) * LIN_ST + jj];
+            if (++m == d) { m = 0; ++jj; }
+          }
+          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int row = nrow0 + m;
+            if (row >= 0 && row < LIN_ROWS) dst[t] = Os[row * LIN_ST + jj];
+            if (++m == d) { m = 0; ++jj; }
+          }
+        }
+        ow.next(jw, d);
+      }
+    } else {
+      Walk3 ow;
+      ow.init(tid, 256, jw, d);
+      for (int f = tid; f < span * olen; f += 256) {
+        const int row = (n_lo + ow.a) * d + ow.m - r0;
+        if (row >= 0 && row < LIN_ROWS) yb[(size_t)ow.a * y_row + ow.b * d + ow.m] = Os[row * LIN_ST + ow.b];
+        ow.next(jw, d);
+      }
     }
   }
 }
