@@ -161,7 +161,7 @@ def main():
     def mlpfb():
         out = mlp(ef)
         out.backward(torch.ones_like(out))
-    rec("radial MLP fwd+bwd (torch)", timeit_if("radial MLP fwd+bwd (torch)", mlpfb, args.reps), None,
+    rec("radial MLP fwd+bwd (nn.Sequential)", timeit_if("radial MLP fwd+bwd (torch)", mlpfb, args.reps), None,
         3 * 2 * e * (12 * 64 + 64 * 64 + 64 * info["wn"]))
     print(json.dumps(res))
 
