@@ -48,8 +48,11 @@ __global__ __launch_bounds__(256) void edge_embed_kernel(
   const float vz = pos[3 * r + 2] - pos[3 * s + 2] + shifts[3 * e + 2];
   const float len = sqrtf(vx * vx + vy * vy + vz * vz);
   const int nsh = (lmax + 1) * (lmax + 1);
-  if (lmax == 4) sh_eval_l4(vx, vy, vz, sh + (size_t)e * nsh);
-  else sh_eval_l3(vx, vy, vz, sh + (size_t)e * nsh);
+  const int nshp = (nsh + 3) & ~3;   // rows padded to 16 B: the TP kernels read them as float4
+  float* __restrict__ she = sh + (size_t)e * nshp;
+  if (lmax == 4) sh_eval_l4(vx, vy, vz, she);
+  else sh_eval_l3(vx, vy, vz, she);
+  for (int j = nsh; j < nshp; ++j) she[j] = 0.0f;
   // soft_one_hot_linspace(x, 0, end, nb, 'gaussian', cutoff=False):
   // values = linspace(0, end, nb); step = values[1]-values[0]; exp(-((x-v)/step)^2)/1.12
   const float rad = radius[e];

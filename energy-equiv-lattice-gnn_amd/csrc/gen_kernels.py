@@ -156,9 +156,51 @@ def _emit_t(p: cg.TPPath, xname, yname, tname, L: List[str], ind: str):
         L.append(f"{ind}const float {tname}{k} = {expr};")
 
 
+_VT = {4: "eelg_f4u", 3: "eelg_f3u", 2: "eelg_f2u"}
+
+
+def vec_load(names: Sequence[str], base: str, start: str) -> List[str]:
+    """names[i] = base[start + i] with dword-aligned 4/3/2-wide loads (start is an expr)."""
+    out, i = [], 0
+    while i < len(names):
+        w = min(4, len(names) - i)
+        if w == 1:
+            out.append(f"{names[i]} = {base}[{start} + {i}];")
+        else:
+            out.append(f"{{ const {_VT[w]} v_ = *reinterpret_cast<const {_VT[w]}*>({base} + {start} + {i}); "
+                       + " ".join(f"{names[i + k]} = v_[{k}];" for k in range(w)) + " }")
+        i += w
+    return out
+
+
+def vec_store(vals: Sequence[str], base: str, start: str) -> List[str]:
+    out, i = [], 0
+    while i < len(vals):
+        w = min(4, len(vals) - i)
+        if w == 1:
+            out.append(f"{base}[{start} + {i}] = {vals[i]};")
+        else:
+            out.append(f"*reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}) = {_VT[w]}{{"
+                       + ", ".join(vals[i: i + w]) + "};")
+        i += w
+    return out
+
+
+def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
+    """the needed SH components from a 16-B aligned padded row, one float4 per 4 components"""
+    need = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
+    out = []
+    for b in sorted({j // 4 for j in need}):
+        comps = [j for j in need if j // 4 == b]
+        out.append(f"{{ const eelg_f4a v_ = *reinterpret_cast<const eelg_f4a*>({base} + {4 * b}); "
+                   + " ".join(f"{pref}y{j} = v_[{j - 4 * b}];" for j in comps) + " }")
+    return out
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, dict]:
     paths = cg.tp_paths(node, sh, target)
     din, nsh = node.dim, sh.dim
+    nshp = (nsh + 3) // 4 * 4              # padded SH row stride (float4 loads)
     irreps_mid = cg.tp_out_irreps_with_instructions(node, sh, target)[0]
     dmid = irreps_mid.dim
     wn = sum(p.mul for p in paths)
@@ -199,19 +241,19 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                + [f"w{p.slot}" for p in grp])
 
         def load(pref, ev, guard):
+            # addresses stay in bounds when the edge does not exist (index 0); the loaded
+            # values of a missing edge are never used
             out = [f"    {{ const bool ok = {guard};",
                    f"      const float* __restrict__ xs = x + (size_t)(ok ? sender[{ev}] : 0) * {din};",
-                   f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nsh};",
+                   f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
                    f"      const float* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
             for l in need_l1:
                 d = 2 * l + 1
-                for i in range(d):
-                    out.append(f"      {pref}x{l}_{i} = ok ? xs[{node_off[l]} + u * {d} + {i}] : 0.0f;")
-            for l in need_l2:
-                for j in range(2 * l + 1):
-                    out.append(f"      {pref}y{l * l + j} = ok ? ye[{l * l + j}] : 0.0f;")
+                out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
+                                                          f"{node_off[l]} + u * {d}")]
+            out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
             for p in grp:
-                out.append(f"      {pref}w{p.slot} = ok ? we[{p.slot * MUL}] : 0.0f;")
+                out.append(f"      {pref}w{p.slot} = we[{p.slot * MUL}];")
             out.append("    }")
             return out
         L.append("    float " + ", ".join(cur) + ";")
@@ -255,7 +297,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     L.append("  const int e = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
     L.append("  if (e >= n_edges) return;")
     L.append("  const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
-    L.append("  const float* __restrict__ ye = sh + (size_t)e * " + str(nsh) + ";")
+    L.append("  const float* __restrict__ ye = sh + (size_t)e * " + str(nshp) + ";")
     L.append("  const float* __restrict__ we = w + (size_t)e * " + str(wn) + " + u;")
     L.append("  float* __restrict__ gwe = gw + (size_t)e * " + str(wn) + " + u;")
     L.append("  const float* __restrict__ ge = gagg + (size_t)receiver[e] * " + str(dmid) + ";")
@@ -265,20 +307,22 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         l = grp[0].l1
         d = 2 * l + 1
         L.append(f"  case {gi}: {{ // input block l1 = {l}")
+        L.append("    float " + ", ".join(f"x{l}_{i}" for i in range(d)) + ";")
+        L += ["    " + ln for ln in vec_load([f"x{l}_{i}" for i in range(d)], "xs", f"{node_off[l]} + u * {d}")]
         for i in range(d):
-            L.append(f"    float x{l}_{i} = xs[{node_off[l]} + u * {d} + {i}];")
             L.append(f"    float gx{l}_{i} = 0.0f;")
         l2s = sorted({p.l2 for p in grp})
-        for l2 in l2s:
-            for j in range(2 * l2 + 1):
-                L.append(f"    float y{l2 * l2 + j} = ye[{l2 * l2 + j}];")
+        L.append("    float " + ", ".join(f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)) + ";")
+        L += ["    " + ln for ln in sh_load(l2s, "", "ye")]
         base_pin = ([f"x{l}_{i}" for i in range(d)] + [f"gx{l}_{i}" for i in range(d)]
                     + [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)])
 
         def pref(p):
             """issue the loads one path needs (its grad_agg slot row and weight)"""
             d3 = 2 * p.l3 + 1
-            out = [f"    float g{p.slot}_{k} = ge[{p.out_off} + u * {d3} + {k}];" for k in range(d3)]
+            out = ["    float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
+            out += ["    " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
+                                                  f"{p.out_off} + u * {d3}")]
             out.append(f"    float w{p.slot} = we[{p.slot * MUL}];")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
         first, _ = pref(grp[0])
@@ -311,8 +355,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                     L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
             L.append("    }")
             L.append("    " + pin(base_pin + nxt_regs))
-        for i in range(d):
-            L.append(f"    gxo[{node_off[l]} + u * {d} + {i}] = gx{l}_{i};")
+        L += ["    " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
@@ -734,7 +777,12 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 def main(outdir: str) -> None:
     os.makedirs(outdir, exist_ok=True)
     parts = ["// GENERATED by csrc/gen_kernels.py -- do not edit", "#include <hip/hip_runtime.h>",
-             "#include <stdint.h>", '#include "../eelg_internal.h"', ""]
+             "#include <stdint.h>", '#include "../eelg_internal.h"', "",
+             "// dword-aligned vector types: per-lane runs of d floats start at 4-byte boundaries",
+             "typedef float eelg_f4u __attribute__((ext_vector_type(4), aligned(4)));",
+             "typedef float eelg_f3u __attribute__((ext_vector_type(3), aligned(4)));",
+             "typedef float eelg_f2u __attribute__((ext_vector_type(2), aligned(4)));",
+             "typedef float eelg_f4a __attribute__((ext_vector_type(4)));", ""]
     for lmax in (3, 4):
         parts.append(emit_sh(lmax))
     tp_table, sc_table = [], []

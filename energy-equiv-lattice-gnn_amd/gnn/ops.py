@@ -108,14 +108,33 @@ def edge_embed(pos, csr: EdgeCSR, shifts_sorted, radius_sorted, lmax: int, nb: i
         raise NotImplementedError("gradients w.r.t. positions are not part of the hot path "
                                   "(the reference never differentiates through geometry)")
     e = csr.num_edges
-    sh = torch.empty(e, (lmax + 1) ** 2, device=pos.device, dtype=torch.float32)
+    nsh = (lmax + 1) ** 2
+    sh = torch.empty(e, sh_row_stride(nsh), device=pos.device, dtype=torch.float32)
     feats = torch.empty(e, 2 * nb, device=pos.device, dtype=torch.float32)
     lib = _lib.load()
     _lib.check(lib.eelg_edge_embed(
         _lib.ptr(_f32(pos)), _lib.ptr(csr.sender), _lib.ptr(csr.receiver),
         _lib.ptr(_f32(shifts_sorted)), _lib.ptr(_f32(radius_sorted)), e, lmax, nb,
         float(len_end), float(rad_end), _lib.ptr(sh), _lib.ptr(feats), _lib.stream()), "edge_embed")
-    return sh, feats
+    return sh[:, :nsh], feats          # [E, nsh] view of the padded rows the TP kernels read
+
+
+def sh_row_stride(nsh: int) -> int:
+    """SH rows are padded to 16 bytes in HBM (float4 loads in the TP kernels)."""
+    return (nsh + 3) // 4 * 4
+
+
+def padded_sh(sh: torch.Tensor) -> torch.Tensor:
+    """The padded-row buffer behind ``sh`` ([E, nsh]): the tensor itself when it is already a
+    view of padded rows (as ``edge_embed`` returns), else a padded copy."""
+    nsh = sh.shape[1]
+    nshp = sh_row_stride(nsh)
+    if (sh.dtype == torch.float32 and sh.stride() == (nshp, 1) and sh.storage_offset() == 0
+            and sh.untyped_storage().nbytes() >= sh.shape[0] * nshp * 4):
+        return sh
+    out = torch.zeros(sh.shape[0], nshp, device=sh.device, dtype=torch.float32)
+    out[:, :nsh] = sh
+    return out[:, :nsh]
 
 
 # ---------------------------------------------------------------------------
@@ -188,7 +207,10 @@ def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
 class _TPInteraction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
-        x, sh, w = _f32(x), _f32(sh), _f32(w)
+        x, w = _f32(x), _f32(w)
+        if sh.dtype != torch.float32:
+            raise TypeError(f"expected float32 SH, got {sh.dtype}")
+        sh = padded_sh(sh)
         n = x.shape[0]
         if x.shape[1] != info["din"] or sh.shape[1] != info["nsh"] or w.shape[1] != info["wn"]:
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} sh {tuple(sh.shape)} "

@@ -9,7 +9,8 @@
  *
  * Layout conventions (reference: gnn/datasets.py:256-269, e3nn mul-major rows):
  *   node features   [N, sum_l mul*(2l+1)]   block (mul, l) laid out [mul][2l+1]
- *   edge SH         [E, (lmax+1)^2]
+ *   edge SH         [E, (lmax+1)^2] in rows padded to a multiple of 4 floats (row stride
+ *                   nshp = round_up((lmax+1)^2, 4): 28 for lmax 4, 16 for lmax 3)
  *   TP weights      [E, npaths*mul]          index = path*mul + channel
  *   edges           receiver-sorted; rowptr[N+1] is the receiver CSR,
  *                   sperm/srowptr the sender CSR over the same edge order.
@@ -45,7 +46,8 @@ int eelg_sc_info(int cfg, int* info6, uint64_t* sig);
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
  * soft_one_hot_linspace x2 + cat (gnn/model.py:146-156) and
  * o3.SphericalHarmonics(lmax, normalize=True, 'component') (gnn/model.py:126-129,157).
- * feats[E, 2*nb] = [gauss(len; 0..len_end) | gauss(radius; 0..rad_end)]. */
+ * sh[E, nshp] (padded rows, pad zeroed), feats[E, 2*nb] =
+ * [gauss(len; 0..len_end) | gauss(radius; 0..rad_end)]. */
 int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, const float* shifts,
                     const float* radius, int n_edges, int lmax, int nb, float len_end,
                     float rad_end, float* sh, float* feats, void* stream);
