@@ -275,8 +275,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
         L.append("    }")
         for p in grp:
             d3 = 2 * p.l3 + 1
-            for k in range(d3):
-                L.append(f"    o[{p.out_off} + u * {d3} + {k}] = a{p.slot}_{k};")
+            L += ["    " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                 f"{p.out_off} + u * {d3}")]
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
