@@ -1,0 +1,141 @@
+"""Full-size and edge-case checks of the HIP path (at BASELINE sizes through
+size-independent properties; edge cases of the graph structure).
+
+The CPU oracle needs ~14 s per 1k-node graph for the 4-layer model, so at BASELINE config 2
+(32 x 1024 nodes / 4096 edges, 4 layers, lmax 4) the checks are invariants:
+* rotation equivariance of the Mandel stiffness (5e-4, as test_gpu_parity),
+* per-graph independence: the 32-graph batch equals each graph alone (1e-4),
+* translation invariance (1e-4) and positive semi-definiteness,
+* training-step gradients match between the batch and the sum of per-graph gradients.
+Edge cases (vs the fp64 oracle, 1e-4): edgeless graphs / isolated nodes, one node with a
+very high in-degree, node counts that do not divide the kernels' tiles, a single graph.
+"""
+import pytest
+import torch
+
+import oracle.model as omodel
+from oracle.train import stiffness_loss as oracle_loss
+
+from helpers import batch_to, copy_params, params
+from helpers_mandel import rotate_mandel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def full():
+    from gnn.data import collate
+    from gnn.model import EnergyEquivGNN
+    from gnn.synthetic import SyntheticLattices
+    ds = SyntheticLattices(32, 1024, 4096, 1234)
+    torch.manual_seed(0)
+    m = EnergyEquivGNN(params(4, max_edge_radius=ds.max_edge_radius)).to(DEV)
+    return m, ds, collate([ds[g] for g in range(32)])
+
+
+def test_fullsize_rotation_translation_psd(full):
+    m, ds, b = full
+    g = torch.Generator().manual_seed(7)
+    q, _ = torch.linalg.qr(torch.randn(3, 3, generator=g, dtype=torch.float64))
+    if torch.det(q) < 0:
+        q[:, 0] = -q[:, 0]
+    with torch.no_grad():
+        c = m(b.to(DEV))["stiffness"].double().cpu()
+        br = b.to(DEV)
+        br.positions = (b.positions.double() @ q.T).float().to(DEV)
+        br.shifts = (b.shifts.double() @ q.T).float().to(DEV)
+        cr = m(br)["stiffness"].double().cpu()
+        bt = b.to(DEV)
+        bt.positions = bt.positions + torch.tensor([0.7, -1.3, 2.9], device=DEV)
+        ct = m(bt)["stiffness"].double().cpu()
+    assert rel_err(cr, rotate_mandel(c, q)) < 5e-4
+    assert rel_err(ct, c) < 1e-4
+    ev = torch.linalg.eigvalsh(c)
+    assert (ev > -1e-5 * ev.abs().max()).all()
+
+
+def test_fullsize_graphs_are_independent(full):
+    from gnn.data import collate
+    m, ds, b = full
+    with torch.no_grad():
+        cb = m(b.to(DEV))["stiffness"]
+        for gi in (0, 13, 31):
+            cs = m(collate([ds[gi]]).to(DEV))["stiffness"]
+            assert rel_err(cb[gi: gi + 1], cs) < 1e-4, gi
+
+
+def test_fullsize_gradient_is_sum_over_graphs(full):
+    """d(sum_g loss_g)/dW from the 32-graph batch == the sum of per-graph gradients."""
+    from gnn.data import collate
+    m, ds, b = full
+    bd = b.to(DEV)
+
+    def grads(batch_):
+        m.zero_grad(set_to_none=True)
+        c = m(batch_)["stiffness"]
+        per = ((c - batch_.stiffness) ** 2).mean(dim=(1, 2)).sum()
+        per.backward()
+        return torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+
+    gb = grads(bd)
+    gs = sum(grads(collate([ds[gi]]).to(DEV)) for gi in range(4))
+    gb4 = grads(collate([ds[gi] for gi in range(4)]).to(DEV))
+    assert rel_err(gb4, gs) < 1e-3
+    assert torch.isfinite(gb).all()
+
+
+def _oracle_pair(b, rmax, layers=2):
+    from gnn.model import EnergyEquivGNN
+    p = params(layers, max_edge_radius=rmax)
+    torch.manual_seed(0)
+    o = omodel.EnergyEquivGNN(p).double()
+    m = EnergyEquivGNN(p).to(DEV)
+    copy_params(o, m)
+    bo = batch_to(b, "cpu", torch.float64)
+    co = o(bo)["stiffness"]
+    oracle_loss(co, bo.stiffness).backward()
+    from gnn.train import stiffness_loss
+    cm = m(b.to(DEV))["stiffness"]
+    stiffness_loss(cm, b.to(DEV).stiffness).backward()
+    worst = max(rel_err(pm.grad, dict(o.named_parameters())[k].grad) for k, pm in m.named_parameters())
+    return rel_err(cm, co), worst
+
+
+def _graph(n, edges, seed=0):
+    """a lattice-like graph with an explicit directed edge list (both directions given)"""
+    from gnn.data import Data
+    g = torch.Generator().manual_seed(seed)
+    e = torch.tensor(edges, dtype=torch.long).T if edges else torch.zeros(2, 0, dtype=torch.long)
+    ne = e.shape[1]
+    a = torch.randn(6, 6, generator=g, dtype=torch.float64)
+    return Data(positions=torch.rand(n, 3, generator=g) * 2.0, node_attrs=torch.ones(n, 1),
+                edge_index=e, shifts=torch.randn(ne, 3, generator=g) * 0.3,
+                edge_attr=torch.rand(ne, 1, generator=g) * 0.04 + 0.005,
+                stiffness=(a @ a.T / 6 + 0.1 * torch.eye(6, dtype=torch.float64)).float())
+
+
+def test_edge_cases_vs_oracle():
+    from gnn.data import collate
+    from gnn.synthetic import SyntheticLattices
+    star = [(s, 0) for s in range(1, 301)] + [(0, s) for s in range(1, 301)]   # in-degree 300
+    graphs = [
+        _graph(5, [], seed=1),                                    # no edges at all
+        _graph(7, [(0, 1), (1, 0), (2, 3), (3, 2)], seed=2),      # isolated nodes 4..6
+        _graph(301, star, seed=3),                                # one hub node
+        SyntheticLattices(1, 37, 142, 5)[0],                     # 37 nodes: no tile divides it
+    ]
+    b = collate(graphs)
+    rmax = float(b.edge_attr.max())
+    err, gerr = _oracle_pair(b, rmax)
+    assert err < 1e-4, err
+    assert gerr < 1e-3, gerr
+    # a single graph, single edge pair
+    b1 = collate([_graph(2, [(0, 1), (1, 0)], seed=9)])
+    err1, gerr1 = _oracle_pair(b1, float(b1.edge_attr.max()))
+    assert err1 < 1e-4 and gerr1 < 1e-3
