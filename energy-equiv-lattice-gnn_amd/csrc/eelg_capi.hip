@@ -229,7 +229,10 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
   if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
   if (n_nodes <= 0) return 0;
   const eelg_tp_cfg& c = t[cfg];
-  dim3 grid((n_nodes + 7) / 8, c.ngroups);
+  // node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up
+  // to a multiple of 8 so every tile's ngroups blocks land on one XCD (see gen_kernels.py)
+  const int tiles = (n_nodes + 8 * c.nph - 1) / (8 * c.nph);
+  dim3 grid(((tiles + 7) / 8) * 8 * c.ngroups);
   hipLaunchKernelGGL(c.fwd, grid, dim3(256), 0, (hipStream_t)stream, x, sh, w, sender, rowptr,
                      n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");

@@ -33,6 +33,12 @@ from gnn import cg  # noqa: E402
 from gnn.irreps import Ir, Irreps  # noqa: E402
 
 MUL = 32
+# receivers per half-wave in tp_fwd (the launcher reads it from the config table)
+TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
+TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
+TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
+TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
+TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
 
 
 fnv1a64 = cg.fnv1a64
@@ -206,7 +212,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     wn = sum(p.mul for p in paths)
     for p in paths:
         assert p.mul == MUL
-    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), 32)
+    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), TP_MAXACC)
     node_ls = [ir.l for _, ir in node]
     node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
     L: List[str] = []
@@ -216,35 +222,43 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     yname = lambda p, j: f"y{p.l2 * p.l2 + j}"  # noqa: E731
 
     # ---------------- forward ----------------
-    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}(")
+    # One half-wave (32 lanes = 32 channels) owns TP_NPH consecutive receivers.  Edges are
+    # receiver-sorted, so their in-edges form ONE contiguous range that the half-wave
+    # streams through with a software pipeline (sender index two edges ahead, the gathered
+    # x / SH / weight row one edge ahead); at each receiver boundary the register
+    # accumulators are stored and reset.  The latency chain rowptr -> sender -> x is paid
+    # once per TP_NPH receivers instead of once per receiver.  Blocks are numbered so that
+    # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
+    # and read the tile's x rows / SH rows / indices through one L2.
+    ng = len(groups)
+    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_WPE})))" if TP_WPE else ""
+    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
-    L.append("  const int node = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
-    L.append("  if (node >= n_nodes) return;")
-    L.append("  const int beg = rowptr[node], end = rowptr[node + 1];")
-    L.append("  float* __restrict__ o = agg + (size_t)node * " + str(dmid) + ";")
-    L.append("  switch (blockIdx.y) {")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
+    L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
+    L.append("  if (n0 >= n_nodes) return;")
+    L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
+    L.append("  switch (grp) {")
     for gi, grp in enumerate(groups):
         L.append(f"  case {gi}: {{")
         need_l1 = sorted({p.l1 for p in grp})
         need_l2 = sorted({p.l2 for p in grp})
-        for p in grp:
-            for k in range(2 * p.l3 + 1):
-                L.append(f"    float a{p.slot}_{k} = 0.0f;")
-        # software-pipelined edge loop: the next edge's sender -> x gather, SH row and
-        # weights are in flight while the current edge computes
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
         cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
                + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
                + [f"w{p.slot}" for p in grp])
 
-        def load(pref, ev, guard):
+        def load(pref, ev, sv, guard):
             # addresses stay in bounds when the edge does not exist (index 0); the loaded
             # values of a missing edge are never used
             out = [f"    {{ const bool ok = {guard};",
-                   f"      const float* __restrict__ xs = x + (size_t)(ok ? sender[{ev}] : 0) * {din};",
+                   f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
                    f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
                    f"      const float* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
             for l in need_l1:
@@ -256,27 +270,56 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                 out.append(f"      {pref}w{p.slot} = we[{p.slot * MUL}];")
             out.append("    }")
             return out
+        L.append("    int e = rowptr[n0];")
+        L.append("    const int eend = rowptr[n1];")
+        L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
+        L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
         L.append("    float " + ", ".join(cur) + ";")
-        L += load("", "beg", "beg < end")
-        L.append("    for (int e = beg; e < end; ++e) {")
-        L.append("      float " + ", ".join("n" + v for v in cur) + ";")
-        L += ["  " + ln for ln in load("n", "e + 1", "e + 1 < end")]
-        gpin = pin([f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)] + cur
-                   + ["n" + v for v in cur])
-        for p in grp:
-            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-            L.append(f"        const float wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
-            _emit_t(p, xname, yname, "t", L, "        ")
-            for k in range(2 * p.l3 + 1):
-                L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
-            L.append("      }")
-            L.append("      " + gpin)
-        L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
-        L.append("    }")
-        for p in grp:
-            d3 = 2 * p.l3 + 1
-            L += ["    " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                 f"{p.out_off} + u * {d3}")]
+        L += load("", "e", "(e < eend ? sender[e] : 0)", "e < eend")
+        gpin = pin(accs + cur)
+        def step(cp, np_):
+            """one pipelined edge step: flush finished receivers, issue edge e+1's loads
+            into the ``np_`` register set, compute edge e from the ``cp`` set"""
+            out = []
+            # flush every receiver whose range ends here (also covers receivers with no in-edges)
+            out.append("      while (node < n1 && nend == e) {")
+            out.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
+            for p in grp:
+                d3 = 2 * p.l3 + 1
+                out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                             f"{p.out_off} + u * {d3}"))
+            out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
+            out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
+            out.append("      }")
+            out.append("      if (e >= eend) break;")
+            out.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
+            out.extend("  " + ln for ln in load(np_, "e + 1", "s1", "e + 1 < eend"))
+            cpin = pin(accs + [cp + v for v in cur] + ([] if TP_NOPIN_NEXT else [np_ + v for v in cur]))
+            xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
+            yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
+            for p in grp:
+                out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+                out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
+                _emit_t(p, xn, yn, "t", out, "        ")
+                for k in range(2 * p.l3 + 1):
+                    out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+                out.append("      }")
+                out.append("      " + cpin)
+            out.append("      s1 = s2; ++e; }")
+            return out
+        if TP_UNROLL2:
+            # two register sets, alternating roles: no end-of-iteration copies
+            L.append("    float " + ", ".join("n" + v for v in cur) + ";")
+            L.append("    for (;;) {")
+            L += step("", "n")
+            L += step("n", "")
+            L.append("    }")
+        else:
+            L.append("    for (;;) {")
+            L.append("      float " + ", ".join("n" + v for v in cur) + ";")
+            L += step("", "n")
+            L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
+            L.append("    }")
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
@@ -361,7 +404,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     L.append("  }")
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
-                npaths=len(paths),
+                npaths=len(paths), nph=TP_NPH,
                 sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
@@ -800,7 +843,7 @@ def main(outdir: str) -> None:
     for name, i in tp_table:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
-                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}}},')
+                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:

@@ -12,7 +12,9 @@ from typing import Dict, Tuple
 
 import torch  # noqa: F401  (loads torch's libamdhip64 first; the .so binds to it by SONAME)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeelg.so")
+# EELG_LIB: an alternative build of the same library (kernel-variant experiments, tools/kbench.py)
+LIB_PATH = os.environ.get("EELG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                      "libeelg.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
