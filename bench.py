@@ -33,7 +33,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def make_params(layers: int, max_edge_radius: float, lmax: int = 4):
+def make_params(layers: int, max_edge_radius: float, lmax: int = 4, storage: str = "float32"):
     from argparse import Namespace
     hid = "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
     ro = "+".join(f"16x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
@@ -42,20 +42,22 @@ def make_params(layers: int, max_edge_radius: float, lmax: int = 4):
                      inter_MLP_dim=64, inter_MLP_layers=3, correlation=3, global_reduction="mean",
                      message_passes=layers, positive_function="matrix_power_2",
                      max_edge_radius=max_edge_radius, lr=1e-3, beta1=0.9, epsilon=1e-8,
-                     amsgrad=True, weight_decay=1e-8)
+                     amsgrad=True, weight_decay=1e-8, storage_dtype=storage)
 
 
-def tp_fwd_bytes(n: int, e: int, din: int, w: int, dmid: int, nsh: int = 25) -> int:
+def tp_fwd_bytes(n: int, e: int, din: int, w: int, dmid: int, nsh: int = 25, wbytes: int = 4) -> int:
     """Algorithmic bytes of one fused-interaction launch ('Fused TP+scatter'):
-    x[N,Din] + sh[E,25] + w[E,W] + sender[E] + rowptr[N+1] (read) + agg[N,Dmid] (write)."""
-    return 4 * (n * din + e * nsh + e * w + e + (n + 1) + n * dmid)
+    x[N,Din] + sh[E,nsh] + w[E,W] + sender[E] + rowptr[N+1] (read) + agg[N,Dmid] (write);
+    w is ``wbytes`` per element (2 with bf16 storage, BASELINE config 5)."""
+    return 4 * (n * din + e * nsh + e + (n + 1) + n * dmid) + wbytes * e * w
 
 
 def pmc_traffic(kernel: str, args) -> dict | None:
     """HBM bytes per launch of ``kernel`` from the committed PMC table (profiles/pmc_traffic.json,
     written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
     of this same default command).  Only valid for the default workload; None otherwise."""
-    if (args.batch, args.nodes, args.edges, args.layers, args.lmax) != (32, 1024, 4096, 4, 4):
+    if (args.batch, args.nodes, args.edges, args.layers, args.lmax, args.storage) != \
+            (32, 1024, 4096, 4, 4, "float32"):
         return None
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -70,7 +72,7 @@ def pmc_traffic(kernel: str, args) -> dict | None:
             "source": f"profiles/pmc_traffic.json ({tab['source']})"}
 
 
-def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
+def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax: int = 4):
     """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
     scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
     shape: fwd + loss + bwd, median over steps within ``budget_s``."""
@@ -81,7 +83,7 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
     ds = SyntheticLattices(1, n_nodes, n_edges, 1234)
     b = collate([ds[0]])
     torch.manual_seed(0)
-    m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius))
+    m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius, lmax))
     times = []
     t_start = time.perf_counter()
     while True:
@@ -96,7 +98,7 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float):
     return {"value": round(1.0 / med, 4), "unit": "lattice-graphs/s", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} edges, "
-                      f"{layers} layers, median of {len(times)} step(s) ({med:.2f} s/step)"}
+                      f"{layers} layers lmax {lmax}, median of {len(times)} step(s) ({med:.2f} s/step)"}
 
 
 def cgc_fwd_bytes(n: int, e: int, d: int) -> int:
@@ -237,7 +239,14 @@ def main():
     ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
     ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"],
                     help="egnn = the headline EnergyEquivGNN; cgc_* = BASELINE config 4 benchmark models")
+    ap.add_argument("--storage", default="float32", choices=["float32", "bfloat16"],
+                    help="storage type of the edge-sized interaction tensors (fp32 arithmetic)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="2 = BASELINE configs[1] (default); 5 = configs[4]: lmax 3, ~5k-node "
+                         "lattices (5000 nodes / 20000 edges), bf16 storage, fp32 accumulate")
     args = ap.parse_args()
+    if args.config == 5:
+        args.lmax, args.nodes, args.edges, args.storage = 3, 5000, 20000, "bfloat16"
     if args.model != "egnn":
         return main_cgc(args)
 
@@ -260,7 +269,7 @@ def main():
     rmax = torch.tensor([max(float(d.edge_attr.max()) for d in mine)], device=dev)
     if world > 1:
         dist.all_reduce(rmax, op=dist.ReduceOp.MAX)
-    params = make_params(args.layers, float(rmax.item()), args.lmax)
+    params = make_params(args.layers, float(rmax.item()), args.lmax, args.storage)
     torch.manual_seed(0)
     model = EnergyEquivGNN(params).to(dev)
     opt = torch.optim.AdamW(model.parameters(), lr=params.lr, betas=(params.beta1, 0.999),
@@ -310,7 +319,8 @@ def main():
         info = lay._config()[1]
         roof = None
         if key in ksum:
-            byts = tp_fwd_bytes(n_tot, e_tot, info["din"], info["wn"], info["dmid"], info["nsh"])
+            byts = tp_fwd_bytes(n_tot, e_tot, info["din"], info["wn"], info["dmid"], info["nsh"],
+                                2 if args.storage == "bfloat16" else 4)
             ms = ksum[key]["mean_ms"]
             ach = byts / (ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -322,15 +332,20 @@ def main():
                 roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget)
+            cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax)
         value = world * args.batch * args.steps / dt
         out = {
-            "metric": "lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU",
+            "metric": ("lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU"
+                       if args.config == 2 else
+                       "lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN lmax 3, ~5k nodes/~20k edges, "
+                       "bf16 storage + fp32 accumulate (BASELINE configs[4])"),
             "value": round(value, 2), "unit": "lattice-graphs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if args.storage == "float32" else "f32 (bf16 storage of w / grad_w / gxe)",
             "data": "synthetic periodic lattices (SURVEY 8d generator), random-init weights",
-            "config": {"workload": f"EnergyEquivGNN {args.layers}-layer lmax{args.lmax}, "
+            "config": {"workload": f"EnergyEquivGNN {args.layers}-layer lmax{args.lmax} "
+                                   f"({args.storage} edge storage), "
                                    f"{args.batch} graphs/GPU x {args.nodes} nodes/{args.edges} edges, "
                                    "fwd+loss+bwd+allreduce+clip+AdamW",
                        "global_batch": args.batch * world, "nodes_per_graph": args.nodes,

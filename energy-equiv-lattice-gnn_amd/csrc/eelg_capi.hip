@@ -72,9 +72,22 @@ __global__ __launch_bounds__(256) void edge_embed_kernel(
 // ---------------------------------------------------------------------------
 // CSR segmented sum: one wave per output row, float4 over the row when aligned
 // ---------------------------------------------------------------------------
-template <bool VEC4>
+// bf16 source rows (bit patterns, BASELINE config 5's edge-sized gradients) are widened
+// exactly to fp32 before the fp32 accumulation.
+__device__ __forceinline__ float4 seg_load4(const float* __restrict__ row, int c) {
+  return reinterpret_cast<const float4*>(row)[c];
+}
+__device__ __forceinline__ float4 seg_load4(const unsigned short* __restrict__ row, int c) {
+  const uint2 v = reinterpret_cast<const uint2*>(row)[c];
+  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                     __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+}
+__device__ __forceinline__ float seg_load1(const float* __restrict__ p) { return *p; }
+__device__ __forceinline__ float seg_load1(const unsigned short* __restrict__ p) { return eelg_bf2f(*p); }
+
+template <bool VEC4, typename T>
 __global__ __launch_bounds__(256) void segment_sum_kernel(
-    const float* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ idx,
+    const T* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ idx,
     const float* __restrict__ row_scale, float scale, int n_rows, int width,
     float* __restrict__ out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -89,7 +102,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int j = beg; j < end; ++j) {
         const int sr = idx ? idx[j] : j;
-        const float4 v = reinterpret_cast<const float4*>(src + (size_t)sr * width)[c];
+        const float4 v = seg_load4(src + (size_t)sr * width, c);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
       acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
@@ -100,7 +113,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
       float acc = 0.f;
       for (int j = beg; j < end; ++j) {
         const int sr = idx ? idx[j] : j;
-        acc += src[(size_t)sr * width + c];
+        acc += seg_load1(src + (size_t)sr * width + c);
       }
       o[c] = acc * sc;
     }
@@ -167,6 +180,23 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+template <typename T>
+static int segment_sum_launch(const T* src, const int* rowptr, const int* idx,
+                              const float* row_scale, float scale, int n_rows, int width,
+                              float* out, void* stream, const char* what) {
+  if (n_rows <= 0 || width <= 0) return 0;
+  dim3 grid((n_rows + 3) / 4);
+  const bool vec = (width % 4 == 0) && ((uintptr_t)src % (4 * sizeof(T)) == 0) &&
+                   ((uintptr_t)out % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL((segment_sum_kernel<true, T>), grid, dim3(256), 0, (hipStream_t)stream, src,
+                       rowptr, idx, row_scale, scale, n_rows, width, out);
+  else
+    hipLaunchKernelGGL((segment_sum_kernel<false, T>), grid, dim3(256), 0, (hipStream_t)stream, src,
+                       rowptr, idx, row_scale, scale, n_rows, width, out);
+  return check_launch(what);
+}
+
 extern "C" {
 
 const char* eelg_version(void) { return EELG_VERSION; }
@@ -222,48 +252,81 @@ int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, co
   return check_launch("edge_embed");
 }
 
-int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
-                const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream) {
+static const eelg_tp_cfg* tp_cfg(int cfg) {
   int n = 0;
   const eelg_tp_cfg* t = eelg_tp_table(&n);
-  if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
-  if (n_nodes <= 0) return 0;
-  const eelg_tp_cfg& c = t[cfg];
-  // node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up
-  // to a multiple of 8 so every tile's ngroups blocks land on one XCD (see gen_kernels.py)
+  if (cfg < 0 || cfg >= n) {
+    fail(-1, "bad tp config %d", cfg);
+    return nullptr;
+  }
+  return &t[cfg];
+}
+
+// node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up to a
+// multiple of 8 so every tile's ngroups blocks land on one XCD (see gen_kernels.py)
+static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes) {
   const int tiles = (n_nodes + 8 * c.nph - 1) / (8 * c.nph);
-  dim3 grid(((tiles + 7) / 8) * 8 * c.ngroups);
-  hipLaunchKernelGGL(c.fwd, grid, dim3(256), 0, (hipStream_t)stream, x, sh, w, sender, rowptr,
-                     n_nodes, inv_norm, agg);
+  return dim3(((tiles + 7) / 8) * 8 * c.ngroups);
+}
+
+int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x, sh,
+                     w, sender, rowptr, n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");
+}
+
+int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
+                     const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x,
+                     sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
+                     agg);
+  return check_launch("tp_fwd_bf16");
 }
 
 int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
                 const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                 float* grad_w, float* gxe, void* stream) {
-  int n = 0;
-  const eelg_tp_cfg* t = eelg_tp_table(&n);
-  if (cfg < 0 || cfg >= n) return fail(-1, "bad tp config %d", cfg);
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
   if (n_edges <= 0) return 0;
-  const eelg_tp_cfg& c = t[cfg];
-  hipLaunchKernelGGL(c.bwd, dim3((n_edges + 7) / 8, c.nbgroups), dim3(256), 0, (hipStream_t)stream, x, sh, w,
-                     sender, receiver, n_edges, grad_agg, inv_norm, grad_w, gxe);
+  hipLaunchKernelGGL(c->bwd, dim3((n_edges + 7) / 8, c->nbgroups), dim3(256), 0,
+                     (hipStream_t)stream, x, sh, w, sender, receiver, n_edges, grad_agg, inv_norm,
+                     grad_w, gxe);
   return check_launch("tp_bwd");
+}
+
+int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
+                     const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                     void* grad_w, void* gxe, void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (n_edges <= 0) return 0;
+  hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 7) / 8, c->nbgroups), dim3(256), 0,
+                     (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sender,
+                     receiver, n_edges, grad_agg, inv_norm, static_cast<unsigned short*>(grad_w),
+                     static_cast<unsigned short*>(gxe));
+  return check_launch("tp_bwd_bf16");
 }
 
 int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
                          const float* row_scale, float scale, int n_rows, int width, float* out,
                          void* stream) {
-  if (n_rows <= 0 || width <= 0) return 0;
-  dim3 grid((n_rows + 3) / 4);
-  const bool vec = (width % 4 == 0) && ((uintptr_t)src % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL(segment_sum_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, src,
-                       rowptr, idx, row_scale, scale, n_rows, width, out);
-  else
-    hipLaunchKernelGGL(segment_sum_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src,
-                       rowptr, idx, row_scale, scale, n_rows, width, out);
-  return check_launch("segment_sum_csr");
+  return segment_sum_launch(src, rowptr, idx, row_scale, scale, n_rows, width, out, stream,
+                            "segment_sum_csr");
+}
+
+int eelg_segment_sum_csr_bf16(const void* src, const int* rowptr, const int* idx,
+                              const float* row_scale, float scale, int n_rows, int width,
+                              float* out, void* stream) {
+  return segment_sum_launch(static_cast<const unsigned short*>(src), rowptr, idx, row_scale, scale,
+                            n_rows, width, out, stream, "segment_sum_csr_bf16");
 }
 
 int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,

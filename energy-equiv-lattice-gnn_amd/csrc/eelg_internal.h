@@ -7,6 +7,12 @@ typedef void (*eelg_tp_fwd_fn)(const float*, const float*, const float*, const i
                                float, float*);
 typedef void (*eelg_tp_bwd_fn)(const float*, const float*, const float*, const int*, const int*, int,
                                const float*, float, float*, float*);
+// bf16 storage (bit patterns in unsigned short) of the edge-sized TP tensors
+typedef void (*eelg_tp_fwd_bf_fn)(const float*, const float*, const unsigned short*, const int*,
+                                  const int*, int, float, float*);
+typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned short*, const int*,
+                                  const int*, int, const float*, float, unsigned short*,
+                                  unsigned short*);
 typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdc_fn)(const float*, const float*, int, int, float*);
@@ -19,6 +25,8 @@ struct eelg_tp_cfg {
   uint64_t sig;
   eelg_tp_fwd_fn fwd;
   eelg_tp_bwd_fn bwd;
+  eelg_tp_fwd_bf_fn fwd_bf;
+  eelg_tp_bwd_bf_fn bwd_bf;
 };
 
 struct eelg_sc_cfg {
@@ -33,4 +41,11 @@ struct eelg_sc_cfg {
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);
+
+// bf16 <-> fp32: the widening is exact; the narrowing rounds to nearest even
+// (v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ float eelg_bf2f(unsigned short v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ unsigned short eelg_f2bf(float f) {
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
+}
 const eelg_sc_cfg* eelg_sc_table(int* n);

@@ -203,7 +203,14 @@ def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
     return out
 
 
-def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, dict]:
+def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
+    """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
+    grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
+    bf = wt == "bf16"
+    sfx = "_bw" if bf else ""
+    WT = "unsigned short" if bf else "float"
+    ld_w = (lambda e: f"eelg_bf2f({e})") if bf else (lambda e: e)   # noqa: E731
+    st_w = (lambda v: f"eelg_f2bf({v})") if bf else (lambda v: v)   # noqa: E731
     paths = cg.tp_paths(node, sh, target)
     din, nsh = node.dim, sh.dim
     nshp = (nsh + 3) // 4 * 4              # padded SH row stride (float4 loads)
@@ -232,8 +239,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
     wpe = f" __attribute__((amdgpu_waves_per_eu({TP_WPE})))" if TP_WPE else ""
-    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
     L.append("  const int lane = threadIdx.x & 63;")
@@ -260,14 +267,14 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
             out = [f"    {{ const bool ok = {guard};",
                    f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
                    f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
-                   f"      const float* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
+                   f"      const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
             for l in need_l1:
                 d = 2 * l + 1
                 out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
                                                           f"{node_off[l]} + u * {d}")]
             out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
             for p in grp:
-                out.append(f"      {pref}w{p.slot} = we[{p.slot * MUL}];")
+                out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             out.append("    }")
             return out
         L.append("    int e = rowptr[n0];")
@@ -330,21 +337,21 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
     # cross-group reduction is needed; grad_w of every path is written once.
     bgroups = [[p for p in paths if p.l1 == l] for l in node_ls]
     bgroups = [g for g in bgroups if g]
-    L.append(f"__global__ __launch_bounds__(256) void tp_bwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append(f"__global__ __launch_bounds__(256) void tp_bwd_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ receiver, int n_edges,")
     L.append("    const float* __restrict__ gagg, float inv_norm,")
-    L.append("    float* __restrict__ gw, float* __restrict__ gxe) {")
+    L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe) {{")
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
     L.append("  const int e = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
     L.append("  if (e >= n_edges) return;")
     L.append("  const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
     L.append("  const float* __restrict__ ye = sh + (size_t)e * " + str(nshp) + ";")
-    L.append("  const float* __restrict__ we = w + (size_t)e * " + str(wn) + " + u;")
-    L.append("  float* __restrict__ gwe = gw + (size_t)e * " + str(wn) + " + u;")
+    L.append(f"  const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
+    L.append(f"  {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
     L.append("  const float* __restrict__ ge = gagg + (size_t)receiver[e] * " + str(dmid) + ";")
-    L.append("  float* __restrict__ gxo = gxe + (size_t)e * " + str(din) + ";")
+    L.append(f"  {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
     L.append("  switch (blockIdx.y) {")
     for gi, grp in enumerate(bgroups):
         l = grp[0].l1
@@ -366,7 +373,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
             out = ["    float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
             out += ["    " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
                                                   f"{p.out_off} + u * {d3}")]
-            out.append(f"    float w{p.slot} = we[{p.slot * MUL}];")
+            out.append(f"    float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
         first, _ = pref(grp[0])
         L += first
@@ -390,7 +397,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                 ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
                 if ts:
                     gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
-            L.append(f"      gwe[{p.slot * MUL}] = cp * ({' + '.join(gterms) if gterms else '0.0f'});")
+            gexpr = " + ".join(gterms) if gterms else "0.0f"
+            L.append(f"      gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
             L.append(f"      const float hw = cp * w{p.slot};")
             for i in range(d1):
                 ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
@@ -398,7 +406,10 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps) -> Tuple[str, d
                     L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
             L.append("    }")
             L.append("    " + pin(base_pin + nxt_regs))
-        L += ["    " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
+        if bf:
+            L += [f"    gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
+        else:
+            L += ["    " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
@@ -832,6 +843,7 @@ def main(outdir: str) -> None:
     for name, (node, sh, target) in tp_configs().items():
         code, info = emit_tp(name, node, sh, target)
         parts.append(code)
+        parts.append(emit_tp(name, node, sh, target, "bf16")[0])
         tp_table.append((name, info))
     for name, (coupling, ls, corr) in sc_configs().items():
         code, info = emit_sc(name, coupling, ls, corr)
@@ -843,7 +855,8 @@ def main(outdir: str) -> None:
     for name, i in tp_table:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
-                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}}},')
+                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
+                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:

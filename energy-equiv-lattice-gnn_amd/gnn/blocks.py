@@ -134,8 +134,11 @@ class TensorProductInteractionBlock(torch.nn.Module):
 
     def __init__(self, node_feats_irreps, edge_attrs_irreps, edge_feats_irreps, irreps_out,
                  agg_norm_const, reduce: str = "sum", bias: bool = False, MLP_dim: int = 64,
-                 MLP_layers: int = 3):
+                 MLP_layers: int = 3, storage_dtype: torch.dtype = torch.float32):
         super().__init__()
+        # bf16: the edge-sized tensors (TP weights, their gradient, per-edge grad of x)
+        # are stored in bf16; all arithmetic stays fp32 (BASELINE config 5)
+        self.storage_dtype = storage_dtype
         self._node_feats_irreps = Irreps(node_feats_irreps)
         self.edge_attrs_irreps = Irreps(edge_attrs_irreps)
         self.edge_feats_irreps = Irreps(edge_feats_irreps)
@@ -183,7 +186,7 @@ class TensorProductInteractionBlock(torch.nn.Module):
         csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
         idx, info = self._config()
         x = self.linear_up(node_feats)
-        w = ops.radial_mlp(edge_feats, self.conv_tp_weights)
+        w = ops.radial_mlp(edge_feats, self.conv_tp_weights, self.storage_dtype)
         agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
         return self.linear(agg), None
 
@@ -194,12 +197,12 @@ class MACELayer(torch.nn.Module):
     def __init__(self, input_irreps, edge_sh_irreps, edge_scalars_irreps, interaction_irreps,
                  output_irreps, interaction_agg_norm_const, interaction_reduction: str,
                  interaction_bias: bool, product_correlation: int, MLP_dim: int = 64,
-                 MLP_layers: int = 3):
+                 MLP_layers: int = 3, storage_dtype: torch.dtype = torch.float32):
         super().__init__()
         self.interaction = TensorProductInteractionBlock(
             input_irreps, edge_sh_irreps, edge_scalars_irreps, interaction_irreps,
             interaction_agg_norm_const, interaction_reduction, interaction_bias, MLP_dim,
-            MLP_layers)
+            MLP_layers, storage_dtype)
         self.product = EquivariantProductBlock(self.interaction.irreps_out, output_irreps,
                                                product_correlation, use_sc=False)
 

@@ -27,6 +27,18 @@ from .irreps import Irreps
 from .o3 import Linear
 
 
+def storage_dtype(params: Namespace) -> torch.dtype:
+    """Optional ``params.storage_dtype`` ('float32' default, or 'bfloat16'): storage type of
+    the edge-sized interaction tensors (BASELINE config 5: bf16 storage, fp32 accumulate).
+    Not a reference field; the reference path is all fp32."""
+    name = str(getattr(params, "storage_dtype", "float32")).replace("torch.", "")
+    table = {"float32": torch.float32, "fp32": torch.float32, "bfloat16": torch.bfloat16,
+             "bf16": torch.bfloat16}
+    if name not in table:
+        raise ValueError(f"storage_dtype {name!r}: expected 'float32' or 'bfloat16'")
+    return table[name]
+
+
 class GNN_Head(torch.nn.Module):  # noqa: N801
     def __init__(self, params: Namespace) -> None:
         super().__init__()
@@ -40,12 +52,13 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         interaction_irreps = (edge_attr_irreps * num_features).sort()[0].simplify()
         readout_irreps = Irreps(params.readout_irreps)
         self.num_interactions = params.message_passes
+        storage = storage_dtype(params)
 
         def layer(inp):
             return MACELayer(inp, edge_attr_irreps, edge_feats_irreps, interaction_irreps, hidden,
                              params.agg_norm_const, params.interaction_reduction, True,
                              params.correlation, MLP_dim=params.inter_MLP_dim,
-                             MLP_layers=params.inter_MLP_layers)
+                             MLP_layers=params.inter_MLP_layers, storage_dtype=storage)
 
         self.layers = torch.nn.ModuleList([layer(node_ft_irreps)])
         for _ in range(self.num_interactions - 1):

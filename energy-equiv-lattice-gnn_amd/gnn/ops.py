@@ -141,14 +141,16 @@ def padded_sh(sh: torch.Tensor) -> torch.Tensor:
 # CSR segmented sum
 # ---------------------------------------------------------------------------
 def segment_sum_csr(src, rowptr, n_rows: int, idx=None, row_scale=None, scale: float = 1.0):
+    """fp32 output; ``src`` is fp32, or bf16 (widened exactly, fp32 accumulation)."""
     _require_device(src)
-    src = _f32(src)
+    bf = src.dtype == torch.bfloat16
+    src = src.contiguous() if bf else _f32(src)
     width = src[0].numel() if src.shape[0] > 0 else int(torch.tensor(src.shape[1:]).prod())
     out = torch.empty((n_rows,) + tuple(src.shape[1:]), device=src.device, dtype=torch.float32)
     lib = _lib.load()
-    _lib.check(lib.eelg_segment_sum_csr(
-        _lib.ptr(src), _lib.ptr(rowptr), _lib.ptr(idx), _lib.ptr(row_scale), float(scale), n_rows,
-        int(width), _lib.ptr(out), _lib.stream()), "segment_sum_csr")
+    fn = lib.eelg_segment_sum_csr_bf16 if bf else lib.eelg_segment_sum_csr
+    _lib.check(fn(_lib.ptr(src), _lib.ptr(rowptr), _lib.ptr(idx), _lib.ptr(row_scale), float(scale),
+                  n_rows, int(width), _lib.ptr(out), _lib.stream()), "segment_sum_csr")
     return out
 
 
@@ -207,7 +209,9 @@ def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
 class _TPInteraction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
-        x, w = _f32(x), _f32(w)
+        # w: fp32, or bf16 storage (BASELINE config 5; fp32 arithmetic in the kernels)
+        bf = w.dtype == torch.bfloat16
+        x, w = _f32(x), (w.contiguous() if bf else _f32(w))
         if sh.dtype != torch.float32:
             raise TypeError(f"expected float32 SH, got {sh.dtype}")
         sh = padded_sh(sh)
@@ -220,9 +224,10 @@ class _TPInteraction(torch.autograd.Function):
         agg = torch.empty(n, info["dmid"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
         tok = TIMER.start(f"tp_fwd[din={info['din']}]")
-        _lib.check(lib.eelg_tp_fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
-                                   _lib.ptr(csr.sender), _lib.ptr(csr.rowptr), n, float(inv_norm),
-                                   _lib.ptr(agg), _lib.stream()), "tp_fwd")
+        fwd = lib.eelg_tp_fwd_bf16 if bf else lib.eelg_tp_fwd
+        _lib.check(fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
+                       _lib.ptr(csr.rowptr), n, float(inv_norm), _lib.ptr(agg), _lib.stream()),
+                   "tp_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, sh, w)
         ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm = csr, cfg, info, inv_norm
@@ -234,14 +239,14 @@ class _TPInteraction(torch.autograd.Function):
         csr, info = ctx.csr, ctx.info
         g = _f32(g)
         e = csr.num_edges
-        gw = torch.empty_like(w)
-        gxe = torch.empty(e, info["din"], device=x.device, dtype=torch.float32)
+        gw = torch.empty_like(w)                       # same storage type as w
+        gxe = torch.empty(e, info["din"], device=x.device, dtype=w.dtype)
         lib = _lib.load()
+        bwd = lib.eelg_tp_bwd_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd
         tok = TIMER.start(f"tp_bwd[din={info['din']}]")
-        _lib.check(lib.eelg_tp_bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
-                                   _lib.ptr(csr.sender), _lib.ptr(csr.receiver), e, _lib.ptr(g),
-                                   float(ctx.inv_norm), _lib.ptr(gw), _lib.ptr(gxe), _lib.stream()),
-                   "tp_bwd")
+        _lib.check(bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
+                       _lib.ptr(csr.receiver), e, _lib.ptr(g), float(ctx.inv_norm), _lib.ptr(gw),
+                       _lib.ptr(gxe), _lib.stream()), "tp_bwd")
         TIMER.stop(tok)
         gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
         return gx, None, gw, None, None, None, None
@@ -318,15 +323,19 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
     (library GEMMs pick no split-K for [64 x 131072] @ [131072 x 64] and run on a few CUs)."""
     e = g.shape[0]
     c = e // chunk
+    acc = torch.promote_types(g.dtype, torch.float32)     # bf16 operands: fp32 sums
     out = None
     if c > 1:
         m = c * chunk
-        out = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2), x[:m].view(c, chunk, -1)).sum(0)
+        # per-chunk partials (bf16 operands: bf16 partials) summed in fp32
+        out = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2),
+                        x[:m].view(c, chunk, -1)).sum(0, dtype=acc)
         g, x = g[m:], x[m:]
     if g.shape[0]:
-        rest = g.t() @ x
+        rest = (g.t() @ x).to(acc)
         out = rest if out is None else out + rest
-    return out if out is not None else torch.zeros(g.shape[1], x.shape[1], device=g.device, dtype=g.dtype)
+    return out if out is not None else torch.zeros(g.shape[1], x.shape[1], device=g.device,
+                                                   dtype=acc)
 
 
 class _RadialMLP(torch.autograd.Function):
@@ -335,7 +344,7 @@ class _RadialMLP(torch.autograd.Function):
     pre-activations; weight gradients use the split-K form above."""
 
     @staticmethod
-    def forward(ctx, feats, *params):
+    def forward(ctx, feats, out_dtype, *params):
         n_hidden = (len(params) - 1) // 2
         h, zs, hs = feats, [], [feats]
         for i in range(n_hidden):
@@ -343,7 +352,12 @@ class _RadialMLP(torch.autograd.Function):
             h = torch.nn.functional.silu(z)
             zs.append(z)
             hs.append(h)
-        out = h @ params[-1].t()
+        if out_dtype == torch.bfloat16:
+            # the [E, W] output layer as a bf16 GEMM (fp32 accumulate), bf16 result
+            hs[-1] = h = h.to(torch.bfloat16)
+            out = h @ params[-1].to(torch.bfloat16).t()
+        else:
+            out = h @ params[-1].t()
         ctx.save_for_backward(*params, *zs, *hs)
         ctx.n_hidden = n_hidden
         return out
@@ -357,19 +371,25 @@ class _RadialMLP(torch.autograd.Function):
         hs = saved[3 * n + 1:]
         g = g.contiguous()
         grads = [None] * len(params)
-        grads[-1] = _wgrad(g, hs[-1])                      # [W, hidden]
-        gh = g @ params[-1]
+        if g.dtype == torch.bfloat16:
+            grads[-1] = _wgrad(g, hs[-1].to(torch.bfloat16)).float()
+            gh = (g @ params[-1].to(torch.bfloat16)).float()
+        else:
+            grads[-1] = _wgrad(g, hs[-1])                  # [W, hidden]
+            gh = g @ params[-1]
         for i in range(n - 1, -1, -1):
             gz = torch.ops.aten.silu_backward(gh, zs[i])
             grads[2 * i] = _wgrad(gz, hs[i])
             grads[2 * i + 1] = gz.sum(0)
             if i > 0:
                 gh = gz @ params[2 * i]
-        return (None, *grads)
+        return (None, None, *grads)
 
 
-def radial_mlp(feats: torch.Tensor, mlp: torch.nn.Sequential) -> torch.Tensor:
-    """Apply ``mlp`` = [Linear(bias), SiLU]*k + [Linear(no bias)] with the fused backward."""
+def radial_mlp(feats: torch.Tensor, mlp: torch.nn.Sequential,
+               out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """Apply ``mlp`` = [Linear(bias), SiLU]*k + [Linear(no bias)] with the fused backward.
+    ``out_dtype`` bf16: the [E, W] output (the TP weights) is stored in bf16."""
     mods = list(mlp)
     params = []
     for i, mod in enumerate(mods):
@@ -383,7 +403,7 @@ def radial_mlp(feats: torch.Tensor, mlp: torch.nn.Sequential) -> torch.Tensor:
         elif not isinstance(mod, torch.nn.SiLU):
             raise ValueError(f"radial MLP: unsupported module {type(mod).__name__}")
     tok = TIMER.start("radial_mlp_fwd")
-    out = _RadialMLP.apply(_f32(feats), *params)
+    out = _RadialMLP.apply(_f32(feats), out_dtype, *params)
     TIMER.stop(tok)
     return out
 

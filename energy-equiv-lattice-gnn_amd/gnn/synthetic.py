@@ -35,12 +35,25 @@ def make_lattice(num_nodes: int, num_edges: int, seed: int) -> Data:
     n = num_nodes
     a = 0.54 * n ** (1.0 / 3.0)
     pos = rng.uniform(0.0, a, size=(n, 3))
-    # all-pairs minimum image distances (n <= a few thousand)
-    d = pos[None, :, :] - pos[:, None, :]          # d[i, j] = pos[j] - pos[i]
-    d, img = _min_image(d, a)
-    dist = np.linalg.norm(d, axis=-1)
-    np.fill_diagonal(dist, np.inf)
-    order = np.argsort(dist, axis=1)
+    # the 8 nearest minimum-image neighbours of every node, in distance order (row blocks of
+    # all-pairs distances; argpartition + sort of the 8 = the first 8 columns of a full argsort)
+    kmax = min(n - 1, 8)
+    order = np.empty((n, kmax), dtype=np.int64)
+    if n > 2048:
+        # large lattices (BASELINE config 5, ~5k nodes): periodic k-d tree, same neighbour set
+        from scipy.spatial import cKDTree
+        _, nb = cKDTree(pos, boxsize=a).query(pos, k=kmax + 1)
+        for i in range(n):
+            row = nb[i][nb[i] != i]
+            order[i] = row[:kmax]
+    for r0 in range(0, n if n <= 2048 else 0, 512):
+        r1 = min(n, r0 + 512)
+        d, _ = _min_image(pos[None, :, :] - pos[r0:r1, None, :], a)   # d[i, j] = pos[j] - pos[i]
+        dist = np.linalg.norm(d, axis=-1)
+        dist[np.arange(r1 - r0), np.arange(r0, r1)] = np.inf
+        part = np.argpartition(dist, kmax - 1, axis=1)[:, :kmax]
+        rows = np.arange(r1 - r0)[:, None]
+        order[r0:r1] = part[rows, np.argsort(dist[rows, part], axis=1, kind="stable")]
     want = num_edges // 2
     pairs = {}
     for i in range(n):
@@ -48,7 +61,6 @@ def make_lattice(num_nodes: int, num_edges: int, seed: int) -> Data:
             key = (min(i, int(j)), max(i, int(j)))
             pairs.setdefault(key, None)
     # top up with random near pairs: i's 3rd..8th nearest neighbours, in random order
-    kmax = min(n - 1, 8)
     cand = [(i, int(order[i, k])) for i in range(n) for k in range(2, kmax)]
     for t in rng.permutation(len(cand)):
         if len(pairs) >= want:
@@ -62,7 +74,7 @@ def make_lattice(num_nodes: int, num_edges: int, seed: int) -> Data:
         keys = [keys[t] for t in sorted(sel)]
     snd = np.array([p[0] for p in keys], dtype=np.int64)
     rcv = np.array([p[1] for p in keys], dtype=np.int64)
-    image = img[snd, rcv]                          # pos[r] - pos[s] + a*image = strut vector
+    _, image = _min_image(pos[rcv] - pos[snd], a)  # pos[r] - pos[s] + a*image = strut vector
     shifts = a * image
     radii = rng.uniform(0.005, 0.05, size=(want, 1))
     edge_index = np.stack([np.concatenate([snd, rcv]), np.concatenate([rcv, snd])])

@@ -64,6 +64,16 @@ int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const 
                 const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                 float* grad_w, float* gxe, void* stream);
 
+/* BASELINE config 5 (bf16 storage, fp32 arithmetic): eelg_tp_fwd / eelg_tp_bwd with the
+ * edge-sized tensors w, grad_w [E, weight_numel] and gxe [E, din] held as bf16 bit patterns
+ * (uint16, round-to-nearest-even on store).  Same reference call sites
+ * (gnn/blocks.py:590-597). */
+int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
+                     const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream);
+int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
+                     const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                     void* grad_w, void* gxe, void* stream);
+
 /* CSR segmented sum (deterministic, no atomics):
  * out[r, :] = scale * row_scale[r] * sum_{j in [rowptr[r], rowptr[r+1])} src[idx ? idx[j] : j, :].
  * Replaces torch_scatter.scatter(..., reduce='sum'|'mean') (gnn/blocks.py:595-597,
@@ -71,6 +81,12 @@ int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const 
 int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
                          const float* row_scale, float scale, int n_rows, int width, float* out,
                          void* stream);
+
+/* eelg_segment_sum_csr over bf16 source rows (bit patterns), fp32 accumulation and output:
+ * the sender sums of the bf16 per-edge gradient gxe (config 5). */
+int eelg_segment_sum_csr_bf16(const void* src, const int* rowptr, const int* idx,
+                              const float* row_scale, float scale, int n_rows, int width,
+                              float* out, void* stream);
 
 /* Few long segments (per-graph pooling): each segment is cut into n_split pieces summed
  * separately into work[n_rows, n_split, width], then combined in a fixed order:

@@ -212,3 +212,13 @@ def test_lmax3_with_l4_hidden_irreps_raises_like_the_reference():
     from gnn.mace import SymmetricContraction
     with pytest.raises(NotImplementedError):
         SymmetricContraction("32x0e+32x1o+32x2e+32x3o", "32x0e+32x1o+32x2e+32x3o+32x4e", 3)
+
+
+def test_storage_dtype_param_validation():
+    """optional params.storage_dtype (BASELINE config 5): float32 default, bfloat16, else raise"""
+    from gnn.model import storage_dtype
+    from helpers import params
+    assert storage_dtype(params(2)) == torch.float32
+    assert storage_dtype(params(2, storage_dtype="bfloat16")) == torch.bfloat16
+    with pytest.raises(ValueError):
+        storage_dtype(params(2, storage_dtype="fp8"))
