@@ -383,7 +383,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -393,7 +393,7 @@ int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x);
   return check_launch("sc_bwd_x");
 }
@@ -413,7 +413,8 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
                      float* partial, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
-  if (chunk <= 0 || chunk % 64) return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of 64");
+  if (chunk <= 0 || chunk % c->nb)
+    return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of %d", c->nb);
   if (n_nodes <= 0) return 0;
   const int nch = (n_nodes + chunk - 1) / chunk;
   hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + c->wpb - 1) / c->wpb, nch, mul), dim3(64 * c->wpb), 0,

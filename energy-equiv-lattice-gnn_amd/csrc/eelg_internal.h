@@ -38,6 +38,7 @@ struct eelg_sc_cfg {
   eelg_sc_bwdc_fn bwd_coef;
   eelg_sc_cmajor_fn cmajor;      // input (coupling) layout
   eelg_sc_cmajor_fn cmajor_out;  // output layout
+  int nb;                        // nodes per fwd / grad-x workgroup and per coef-grad tile
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -38,6 +38,11 @@ TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
 TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
 TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
+# symmetric contraction: nodes per lane.  2 = packed-fp32 v_pk_* arithmetic on node pairs;
+# measured slower than 1 on MI355X (fwd 0.45 vs 0.35 ms, grad-x 0.76 vs 0.56, coef-grad 1.16 vs
+# 0.86): twice the VGPRs and LDS per workgroup halve the occupancy, the SGPR coefficient
+# operands need aligned pairs (s_mov per term), and dependent v_pk ops carry a wait state
+SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
 TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
 
 
@@ -527,25 +532,47 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    def stage_in(src, tile, lay):
-        per = (64 * lay.QD + 255) // 256
+    PKN = SC_PK
+    NB = 64 * PKN                           # nodes per workgroup (fwd / grad-x)
+    FT = "float" if PKN == 1 else "eelg_f2"
+    ZERO = "0.0f" if PKN == 1 else "eelg_f2{0.0f, 0.0f}"
+
+    def fma_s(c, v, acc):
+        """acc + c * v, c a wave-uniform scalar coefficient"""
+        return f"fmaf({c}, {v}, {acc})" if PKN == 1 else f"eelg_fma2s({c}, {v}, {acc})"
+
+    def fma_v(a, b, acc):
+        return f"fmaf({a}, {b}, {acc})" if PKN == 1 else f"eelg_fma2({a}, {b}, {acc})"
+
+    def ld_pair(dst, base0, base1, col):
+        if PKN == 1:
+            return f"{FT} {dst} = {base0}[{col}];"
+        return f"{FT} {dst} = eelg_f2{{{base0}[{col}], {base1}[{col}]}};"
+
+    def st_pair(val, base0, base1, col):
+        if PKN == 1:
+            return f"{base0}[{col}] = {val};"
+        return f"{base0}[{col}] = {val}.x; {base1}[{col}] = {val}.y;"
+
+    def stage_in(src, tile, lay, nb=64):
+        per = (nb * lay.QD + 255) // 256
         out = ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                "#pragma unroll 2",
                f"  for (int it = 0; it < {per}; ++it) {{",
                f"    const int idx = tid + 256 * it;",
-               f"    if (idx < {64 * lay.QD}) {{",
+               f"    if (idx < {nb * lay.QD}) {{",
                f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
                f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] : 0.0f;",
                "    }", "  } }"]
         return out
 
-    def stage_out(dst, tile, lay):
-        per = (64 * lay.QD + 255) // 256
+    def stage_out(dst, tile, lay, nb=64):
+        per = (nb * lay.QD + 255) // 256
         return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                 "#pragma unroll 2",
                 f"  for (int it = 0; it < {per}; ++it) {{",
                 f"    const int idx = tid + 256 * it;",
-                f"    if (idx < {64 * lay.QD}) {{",
+                f"    if (idx < {nb * lay.QD}) {{",
                 f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
                 f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = {tile}[nl * {TP} + q];",
                 "    }", "  } }"]
@@ -563,7 +590,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             else:
                 g["d3"].setdefault(c, []).append((t, q))
 
-    head = ["  const int cq = blockIdx.x;", "  const int n0 = blockIdx.y * 64;",
+    head = ["  const int cq = blockIdx.x;", f"  const int n0 = blockIdx.y * {NB};",
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + wv);",
             f"  const int cl = __builtin_amdgcn_readfirstlane(wv);",
@@ -573,15 +600,18 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
-    L.append(f"  __shared__ float tile[64 * {TP}];")
+    L.append(f"  __shared__ float tile[{NB} * {TP}];")
     L += head
-    L += stage_in("x", "tile", lin)
+    L += stage_in("x", "tile", lin, NB)
     L.append("  __syncthreads();")
+    # packed: a lane owns nodes n0 + lane and n0 + 64 + lane (one v_pk_* op covers both)
     L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
+    if PKN == 2:
+        L.append(f"  float* __restrict__ tr1 = tile + (lane + 64) * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = tr[{lq(lin, a, 'cl')}];")
+        L.append("  " + ld_pair(f"x{a}", "tr", "tr1", lq(lin, a, 'cl')))
     for q in range(Dout):
-        L.append(f"  float o{q} = 0.0f;")
+        L.append(f"  {FT} o{q} = {ZERO};")
     blocks = sc_blocks(plan)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
     for t in blocks[0]["terms"]:
@@ -593,27 +623,27 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
+                L.append(f"  o{q} = {fma_s(f'c{t}', f'x{a}', f'o{q}')};")
         else:
             a, b = blk["a"], blk["b"]
             pv = f"p{a}_{b}"
             if blk["first"]:
-                L.append(f"  float {pv} = x{a} * x{b};")
+                L.append(f"  {FT} {pv} = x{a} * x{b};")
             for t, q in blk["d2"]:
-                L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
+                L.append(f"  o{q} = {fma_s(f'c{t}', pv, f'o{q}')};")
             for cc, lst in blk["d3"]:
-                L.append(f"  {{ const float m = {pv} * x{cc};")
+                L.append(f"  {{ const {FT} m = {pv} * x{cc};")
                 for t, q in lst:
-                    L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
+                    L.append(f"    o{q} = {fma_s(f'c{t}', 'm', f'o{q}')};")
                 L.append("  }")
             if not blk["last"]:
                 carry = [pv]
         L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for q in range(Dout):
-        L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
+        L.append("  " + st_pair(f"o{q}", "tr", "tr1", lq(lout, q, 'cl')))
     L.append("  __syncthreads();")
-    L += stage_out("out", "tile", lout)
+    L += stage_out("out", "tile", lout, NB)
     L.append("}")
 
     # ---------------- backward w.r.t. x ----------------
@@ -622,19 +652,21 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx) {")
     # one LDS tile, used three times (x in, grad_out in, grad_x out): 2x the occupancy of
     # separate x / grad_out tiles
-    L.append(f"  __shared__ float tx[64 * {TP}];")
+    L.append(f"  __shared__ float tx[{NB} * {TP}];")
     L += head
-    L += stage_in("x", "tx", lin)
+    L += stage_in("x", "tx", lin, NB)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
+    if PKN == 2:
+        L.append(f"  float* __restrict__ xr1 = tx + (lane + 64) * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = xr[{lq(lin, a, 'cl')}];")
-        L.append(f"  float d{a} = 0.0f;")
+        L.append("  " + ld_pair(f"x{a}", "xr", "xr1", lq(lin, a, 'cl')))
+        L.append(f"  {FT} d{a} = {ZERO};")
     L.append("  __syncthreads();")
-    L += stage_in("gout", "tx", lout)
+    L += stage_in("gout", "tx", lout, NB)
     L.append("  __syncthreads();")
     for q in range(Dout):
-        L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
+        L.append("  " + ld_pair(f"g{q}", "xr", "xr1", lq(lout, q, 'cl')))
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     for t in blocks[0]["terms"]:
         L.append(f"  float c{t} = cf[{t}];")
@@ -645,29 +677,29 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
+                L.append(f"  d{a} = {fma_s(f'c{t}', f'g{q}', f'd{a}')};")
         else:
             a, b = blk["a"], blk["b"]
             pv, sv = f"p{a}_{b}", f"s{a}_{b}"
             if blk["first"]:
-                L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
+                L.append(f"  {FT} {pv} = x{a} * x{b}; {FT} {sv} = {ZERO};")
             for t, q in blk["d2"]:
-                L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
+                L.append(f"  {sv} = {fma_s(f'c{t}', f'g{q}', sv)};")
             for cc, lst in blk["d3"]:
-                L.append("  { float s = 0.0f;")
+                L.append(f"  {{ {FT} s = {ZERO};")
                 for t, q in lst:
-                    L.append(f"    s = fmaf(c{t}, g{q}, s);")
-                L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
+                    L.append(f"    s = {fma_s(f'c{t}', f'g{q}', 's')};")
+                L.append(f"    d{cc} = {fma_v('s', pv, f'd{cc}')}; {sv} = {fma_v('s', f'x{cc}', sv)}; }}")
             if blk["last"]:
-                L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
+                L.append(f"  d{a} = {fma_v(sv, f'x{b}', f'd{a}')}; d{b} = {fma_v(sv, f'x{a}', f'd{b}')};")
             else:
                 carry = [pv, sv]
         L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for a in range(D):
-        L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
+        L.append("  " + st_pair(f"d{a}", "xr", "xr1", lq(lin, a, 'cl')))
     L.append("  __syncthreads();")
-    L += stage_out("gx", "tx", lin)
+    L += stage_out("gx", "tx", lin, NB)
     L.append("}")
 
     # ---------------- mul-major -> channel-major transpose ----------------
@@ -704,7 +736,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         emit_cmajor(cmajor_out, lout)
 
     # ---------------- backward w.r.t. coefficients ----------------
-    JG = 64
+    JG = 64 if PKN == 1 else 32               # terms per wave (packed: 2 nodes per accumulator)
+    NBC = 64 * PKN                            # nodes per staged tile
     WPB = 8                                   # waves (term groups) per workgroup
     groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
     L.append(f"// coefficient gradient from channel-major x / g: {len(groups)} term groups of <= {JG};")
@@ -713,8 +746,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"__global__ __launch_bounds__({64 * WPB}) void sc_bwd_coef_{name}(")
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
-    L.append(f"  __shared__ float sx[{D} * 64];")
-    L.append(f"  __shared__ float sg[{Dout} * 64];")
+    L.append(f"  __shared__ float sx[{D} * {NBC}];")
+    L.append(f"  __shared__ float sg[{Dout} * {NBC}];")
     L.append("  const int c = blockIdx.z;")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
     L.append(f"  const int jg = __builtin_amdgcn_readfirstlane(blockIdx.x * {WPB} + wv);")
@@ -722,33 +755,33 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  const float* __restrict__ gs = gt + (size_t)c * {Dout} * n_nodes;")
     L.append("  const int nb = blockIdx.y * chunk;")
     L.append("  const int ne = min(n_nodes, nb + chunk);")
-    L.append(f"  float acc[{JG}];")
+    L.append(f"  {FT} acc[{JG}];")
     L.append("#pragma unroll")
-    L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = 0.0f;")
+    L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = {ZERO};")
     # double-buffered staging: the next tile's global loads are in flight (in
     # registers) while the current tile is consumed from LDS
-    per = (max(D, Dout) * 64 + 64 * WPB - 1) // (64 * WPB)
+    per = (max(D, Dout) * NBC + 64 * WPB - 1) // (64 * WPB)
     for it in range(per):
         L.append(f"  float rx{it} = 0.0f, rg{it} = 0.0f;")
 
     def issue(base):
         out = []
         for it in range(per):
-            out.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; const int a = idx >> 6, n = {base} + (idx & 63);")
-            out.append(f"      rx{it} = (idx < {D * 64} && n < ne) ? xs[(size_t)a * n_nodes + n] : 0.0f;"
-                       f" rg{it} = (idx < {Dout * 64} && n < ne) ? gs[(size_t)a * n_nodes + n] : 0.0f; }}")
+            out.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; const int a = idx >> {NBC.bit_length() - 1}, n = {base} + (idx & {NBC - 1});")
+            out.append(f"      rx{it} = (idx < {D * NBC} && n < ne) ? xs[(size_t)a * n_nodes + n] : 0.0f;"
+                       f" rg{it} = (idx < {Dout * NBC} && n < ne) ? gs[(size_t)a * n_nodes + n] : 0.0f; }}")
         return out
     L += issue("nb")
 
     def tile_loop(body):
         """the 64-node tile loop; every wave of the workgroup runs it (same barrier count)"""
-        out = ["      for (int n0 = nb; n0 < ne; n0 += 64) {"]
+        out = [f"      for (int n0 = nb; n0 < ne; n0 += {NBC}) {{"]
         for it in range(per):
-            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * 64}) sx[idx] = rx{it};"
-                       f" if (idx < {Dout * 64}) sg[idx] = rg{it}; }}")
+            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * NBC}) sx[idx] = rx{it};"
+                       f" if (idx < {Dout * NBC}) sg[idx] = rg{it}; }}")
         out.append("        __syncthreads();")
-        out.append("        if (n0 + 64 < ne) {")
-        out += ["    " + ln for ln in issue("n0 + 64")]
+        out.append(f"        if (n0 + {NBC} < ne) {{")
+        out += ["    " + ln for ln in issue(f"n0 + {NBC}")]
         out.append("        }")
         out += body
         out.append("        __syncthreads();")
@@ -770,27 +803,28 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             if nu >= 3:
                 need_x.add(cc)
         body = []
+        # packed: a lane owns the adjacent nodes 2 * lane, 2 * lane + 1 of the tile (ds_read_b64)
         for a in sorted(need_x):
-            body.append(f"        const float x{a} = sx[{a * 64} + lane];")
+            body.append(f"        const {FT} x{a} = *reinterpret_cast<const {FT}*>(&sx[{a * NBC} + {PKN} * lane]);")
         for q in sorted(need_g):
-            body.append(f"        const float g{q} = sg[{q * 64} + lane];")
+            body.append(f"        const {FT} g{q} = *reinterpret_cast<const {FT}*>(&sg[{q * NBC} + {PKN} * lane]);")
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         cur = None
         for jj, t in enumerate(grp):
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
-                body.append(f"        acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
+                body.append(f"        acc[{jj}] = {fma_v(f'x{a}', f'g{q}', f'acc[{jj}]')};")
                 continue
             if cur != (a, b):
                 if cur is not None:
                     body.append("        }")
                     body.append("        " + cpin)
-                body.append(f"        {{ const float p = x{a} * x{b};")
+                body.append(f"        {{ const {FT} p = x{a} * x{b};")
                 cur = (a, b)
             if nu == 2:
-                body.append(f"          acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
+                body.append(f"          acc[{jj}] = {fma_v('p', f'g{q}', f'acc[{jj}]')};")
             else:
-                body.append(f"          acc[{jj}] = fmaf(p * x{cc}, g{q}, acc[{jj}]);")
+                body.append(f"          acc[{jj}] = {fma_v(f'p * x{cc}', f'g{q}', f'acc[{jj}]')};")
         if cur is not None:
             body.append("        }")
         body.append("        " + cpin)
@@ -800,29 +834,37 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L += tile_loop([])
     L.append("      break; }")
     L.append("  }")
-    # recursive-halving reduction over the 6 lane bits: with R = JG / 64 values left
-    # per lane, lane L ends with terms R*L + i (i < R)
-    assert JG % 64 == 0
+    # recursive-halving reduction over the lane bits: each step trades half of the values
+    # with the partner lane (bit b), so after log2(JG) steps (bits 32, 16, ...) lane L holds
+    # term L >> (6 - log2(JG)); the remaining low lane bits are summed by butterflies
+    k = JG.bit_length() - 1
+    assert 1 << k == JG and k <= 6
+    red = "acc" if PKN == 1 else "red"
+    if PKN == 2:
+        L.append(f"  float red[{JG}];")
+        L.append(f"  for (int i = 0; i < {JG}; ++i) red[i] = acc[i].x + acc[i].y;")
     n = JG
-    for bit in (32, 16, 8, 4, 2, 1):
+    bits = [32, 16, 8, 4, 2, 1]
+    for bit in bits[:k]:
         h = n // 2
         L.append(f"  {{ const bool up = (lane & {bit}) != 0;")
         for i in range(h):
-            L.append(f"    {{ const float keep = up ? acc[{i + h}] : acc[{i}]; "
-                     f"const float give = up ? acc[{i}] : acc[{i + h}]; "
-                     f"acc[{i}] = keep + __shfl_xor(give, {bit}); }}")
+            L.append(f"    {{ const float keep = up ? {red}[{i + h}] : {red}[{i}]; "
+                     f"const float give = up ? {red}[{i}] : {red}[{i + h}]; "
+                     f"{red}[{i}] = keep + __shfl_xor(give, {bit}); }}")
             if i % 8 == 7:
-                L.append("    " + pin([f"acc[{t}]" for t in range(i - 7, i + 1)], memory=False))
+                L.append("    " + pin([f"{red}[{t}]" for t in range(i - 7, i + 1)], memory=False))
         L.append("  }")
         n = h
-    R = JG // 64
-    L.append(f"  if (jg < {len(groups)}) {{")
+    for bit in bits[k:]:
+        L.append(f"  {red}[0] += __shfl_xor({red}[0], {bit});")
+    low = (1 << (6 - k)) - 1
+    L.append(f"  if (jg < {len(groups)} && (lane & {low}) == 0) {{")
     L.append(f"    float* __restrict__ dst = part + ((size_t)blockIdx.y * {MUL} + c) * {nt};")
-    for i in range(R):
-        L.append(f"    {{ const int t = jg * {JG} + {R} * lane + {i}; if (t < {nt}) dst[t] = acc[{i}]; }}")
+    L.append(f"    const int t = jg * {JG} + (lane >> {6 - k}); if (t < {nt}) dst[t] = {red}[0];")
     L.append("  }")
     L.append("}")
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -836,7 +878,13 @@ def main(outdir: str) -> None:
              "typedef float eelg_f4u __attribute__((ext_vector_type(4), aligned(4)));",
              "typedef float eelg_f3u __attribute__((ext_vector_type(3), aligned(4)));",
              "typedef float eelg_f2u __attribute__((ext_vector_type(2), aligned(4)));",
-             "typedef float eelg_f4a __attribute__((ext_vector_type(4)));", ""]
+             "typedef float eelg_f4a __attribute__((ext_vector_type(4)));",
+             "// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two fp32 lanes per instruction)",
+             "typedef float eelg_f2 __attribute__((ext_vector_type(2)));",
+             "__device__ __forceinline__ eelg_f2 eelg_fma2(eelg_f2 a, eelg_f2 b, eelg_f2 c) {"
+             " return __builtin_elementwise_fma(a, b, c); }",
+             "__device__ __forceinline__ eelg_f2 eelg_fma2s(float a, eelg_f2 b, eelg_f2 c) {"
+             " return __builtin_elementwise_fma(eelg_f2{a, a}, b, c); }", ""]
     for lmax in (3, 4):
         parts.append(emit_sh(lmax))
     tp_table, sc_table = [], []
@@ -862,7 +910,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}}},')
+                     f'{i["cmajor_out"]}, {i["nb"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")
