@@ -390,11 +390,16 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
 
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
                   int mul, float* grad_x, void* stream) {
+  return eelg_sc_bwd_x_cm(cfg, x, coef, grad_out, n_nodes, mul, grad_x, nullptr, nullptr, stream);
+}
+
+int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* grad_out,
+                     int n_nodes, int mul, float* grad_x, float* xt, float* gt, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
   hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
-                     (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x);
+                     (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
 }
 

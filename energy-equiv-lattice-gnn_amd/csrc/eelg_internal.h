@@ -14,7 +14,8 @@ typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned sho
                                   const int*, int, const float*, float, unsigned short*,
                                   unsigned short*);
 typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
-typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*);
+typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*, float*,
+                                float*);
 typedef void (*eelg_sc_bwdc_fn)(const float*, const float*, int, int, float*);
 typedef void (*eelg_sc_cmajor_fn)(const float*, int, float*);
 

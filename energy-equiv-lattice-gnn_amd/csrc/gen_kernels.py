@@ -577,6 +577,26 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = {tile}[nl * {TP} + q];",
                 "    }", "  } }"]
 
+    def cm_store(dst, tile, lay, nb, ind="  "):
+        """dst[(c * D + a) * n_nodes + n] = component a of channel c of node n, from a staged
+        tile of nb nodes x the quad's 4 channels (coalesced nb-float runs per (c, a))"""
+        dd = lay.D
+        sgs = ", ".join(str(lay.comp[a][3]) for a in range(dd))
+        dls = ", ".join(str(2 * lay.comp[a][0] + 1) for a in range(dd))
+        ms = ", ".join(str(lay.comp[a][1]) for a in range(dd))
+        sh = nb.bit_length() - 1
+        per = (Q * dd * nb + 255) // 256
+        out = [f"{{ const int kseg[{dd}] = {{{sgs}}}, kd[{dd}] = {{{dls}}}, km[{dd}] = {{{ms}}};",
+               f"  for (int it = 0; it < {per}; ++it) {{",
+               "    const int idx = threadIdx.x + 256 * it;",
+               f"    if (idx < {Q * dd * nb}) {{",
+               f"      const int row = idx >> {sh}, nl = idx & {nb - 1}, n = n0 + nl;",
+               f"      const int cl = row / {dd}, a = row - cl * {dd};",
+               f"      if (n < n_nodes) {dst}[(size_t)((cq * {Q} + cl) * {dd} + a) * n_nodes + n] = "
+               f"{tile}[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];",
+               "    }", "  } }"]
+        return [ind + ln for ln in out]
+
     # group terms by (a, b) pair
     pairs: Dict[Tuple[int, int], Dict] = {}
     deg1 = []
@@ -649,13 +669,18 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # ---------------- backward w.r.t. x ----------------
     L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
-    L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx) {")
+    L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
+    L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
     # one LDS tile, used three times (x in, grad_out in, grad_x out): 2x the occupancy of
-    # separate x / grad_out tiles
+    # separate x / grad_out tiles.  When xt / gt are given, the staged tiles are also written
+    # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
     L.append(f"  __shared__ float tx[{NB} * {TP}];")
     L += head
     L += stage_in("x", "tx", lin, NB)
     L.append("  __syncthreads();")
+    L.append("  if (xt) {")
+    L += cm_store("xt", "tx", lin, NB, "    ")
+    L.append("  }")
     L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
     if PKN == 2:
         L.append(f"  float* __restrict__ xr1 = tx + (lane + 64) * {TP};")
@@ -665,6 +690,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  __syncthreads();")
     L += stage_in("gout", "tx", lout, NB)
     L.append("  __syncthreads();")
+    L.append("  if (gt) {")
+    L += cm_store("gt", "tx", lout, NB, "    ")
+    L.append("  }")
     for q in range(Dout):
         L.append("  " + ld_pair(f"g{q}", "xr", "xr1", lq(lout, q, 'cl')))
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
@@ -713,21 +741,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append("  const int n0 = blockIdx.y * 64;")
         L.extend(stage_in("x", "tile", lay))
         L.append("  __syncthreads();")
-        dd = lay.D
-        sgs = ", ".join(str(lay.comp[a][3]) for a in range(dd))
-        dls = ", ".join(str(2 * lay.comp[a][0] + 1) for a in range(dd))
-        ms = ", ".join(str(lay.comp[a][1]) for a in range(dd))
-        L.append(f"  const int kseg[{dd}] = {{{sgs}}}, kd[{dd}] = {{{dls}}}, km[{dd}] = {{{ms}}};")
-        per = (Q * dd * 64 + 255) // 256
-        L.append(f"  for (int it = 0; it < {per}; ++it) {{")
-        L.append("    const int idx = threadIdx.x + 256 * it;")
-        L.append(f"    if (idx < {Q * dd * 64}) {{")
-        L.append("      const int row = idx >> 6, nl = idx & 63, n = n0 + nl;")
-        L.append(f"      const int cl = row / {dd}, a = row - cl * {dd};")
-        L.append(f"      if (n < n_nodes) xt[(size_t)((cq * {Q} + cl) * {dd} + a) * n_nodes + n] = "
-                 f"tile[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];")
-        L.append("    }")
-        L.append("  }")
+        L.extend(cm_store("xt", "tile", lay, 64))
         L.append("}")
     emit_cmajor(f"sc_cmajor_{name}", lin)
     cmajor_out = f"sc_cmajor_{name}"

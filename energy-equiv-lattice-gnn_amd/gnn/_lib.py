@@ -40,6 +40,7 @@ _SIGS = {
     "eelg_csr_spmm": ([_P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P], _I),
     "eelg_sc_fwd": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),
+    "eelg_sc_bwd_x_cm": ([_I, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
     "eelg_sc_cmajor": ([_I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),

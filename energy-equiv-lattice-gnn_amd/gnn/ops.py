@@ -284,21 +284,28 @@ class _SymCon(torch.autograd.Function):
         n = x.shape[0]
         lib = _lib.load()
         gx = gcoef = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.empty_like(x)
-            tok = TIMER.start("sc_bwd_x")
-            _lib.check(lib.eelg_sc_bwd_x(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
-                                         ctx.mul, _lib.ptr(gx), _lib.stream()), "sc_bwd_x")
-            TIMER.stop(tok)
-        if ctx.needs_input_grad[1]:
+        want_x, want_c = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if want_c:
             xt = torch.empty(ctx.mul * ctx.info["D"], n, device=x.device, dtype=torch.float32)
             gt = torch.empty(ctx.mul * ctx.info["Dout"], n, device=x.device, dtype=torch.float32)
-            tok = TIMER.start("sc_cmajor")
-            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
-                                          _lib.stream()), "sc_cmajor")
-            _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
-                                          _lib.stream()), "sc_cmajor")
+        if want_x:
+            # grad-x; its staged tiles also give the channel-major operands of the coef-grad
+            gx = torch.empty_like(x)
+            tok = TIMER.start("sc_bwd_x")
+            _lib.check(lib.eelg_sc_bwd_x_cm(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
+                                            ctx.mul, _lib.ptr(gx),
+                                            _lib.ptr(xt) if want_c else None,
+                                            _lib.ptr(gt) if want_c else None, _lib.stream()),
+                       "sc_bwd_x")
             TIMER.stop(tok)
+        if want_c:
+            if not want_x:
+                tok = TIMER.start("sc_cmajor")
+                _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
+                                              _lib.stream()), "sc_cmajor")
+                _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
+                                              _lib.stream()), "sc_cmajor")
+                TIMER.stop(tok)
             chunk = max(128, min(4096, (n // 16 + 127) // 128 * 128))   # a multiple of the tile
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)

@@ -128,6 +128,11 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
                   int mul, float* grad_x, void* stream);
+/* eelg_sc_bwd_x that also writes the channel-major copies xt[(c*D + a)*N + n] of x and
+ * gt[(c*D_out + q)*N + n] of grad_out (the operands of eelg_sc_bwd_coef) from the tiles it
+ * stages anyway, replacing two eelg_sc_cmajor passes; xt / gt may be NULL. */
+int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* grad_out,
+                     int n_nodes, int mul, float* grad_x, float* xt, float* gt, void* stream);
 /* Channel-major copy xt[(c*D + a)*N + n] of a mul-major row tensor (feeds sc_bwd_coef);
  * which = 0: input (coupling) layout, 1: output layout. */
 int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,

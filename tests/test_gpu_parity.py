@@ -273,3 +273,32 @@ def test_irreps_linear_fwd_bwd(irreps_in, irreps_out, bias, n):
     assert rel_err(m.weight.grad, o.weight.grad) < 5e-6
     if bias:
         assert rel_err(m.bias.grad, o.bias.grad) < 5e-6
+
+
+@pytest.mark.parametrize("n", [1000, 64, 7])
+def test_symcon_grad_x_writes_channel_major_copies(n):
+    """eelg_sc_bwd_x_cm: grad-x identical to eelg_sc_bwd_x, and its channel-major copies of x
+    and grad_out identical (bit-exact copies) to the eelg_sc_cmajor transposes."""
+    from gnn import _lib
+    from gnn.mace import SymmetricContraction
+    torch.manual_seed(2)
+    hid = "32x0e+32x1o+32x2e+32x3o+32x4e"
+    sc = SymmetricContraction(hid, hid, 3).to(DEV)
+    idx, info = sc._config()
+    coef = sc.coefficients().detach()
+    x = torch.randn(n, 800, device=DEV)
+    g = torch.randn(n, 800, device=DEV)
+    lib = _lib.load()
+    gx0, gx1 = torch.empty_like(x), torch.empty_like(x)
+    xt0, gt0 = torch.empty(800, n, device=DEV), torch.empty(800, n, device=DEV)
+    xt1, gt1 = torch.full((800, n), 7.0, device=DEV), torch.full((800, n), 7.0, device=DEV)
+    s = _lib.stream()
+    _lib.check(lib.eelg_sc_bwd_x(idx, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n, 32,
+                                 _lib.ptr(gx0), s), "bwd_x")
+    _lib.check(lib.eelg_sc_cmajor(idx, 0, _lib.ptr(x), n, 32, _lib.ptr(xt0), s), "cm")
+    _lib.check(lib.eelg_sc_cmajor(idx, 1, _lib.ptr(g), n, 32, _lib.ptr(gt0), s), "cm")
+    _lib.check(lib.eelg_sc_bwd_x_cm(idx, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n, 32,
+                                    _lib.ptr(gx1), _lib.ptr(xt1), _lib.ptr(gt1), s), "bwd_x_cm")
+    torch.cuda.synchronize()
+    assert torch.equal(gx0, gx1)
+    assert torch.equal(xt0, xt1) and torch.equal(gt0, gt1)
