@@ -239,6 +239,8 @@ def main():
     ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
     ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"],
                     help="egnn = the headline EnergyEquivGNN; cgc_* = BASELINE config 4 benchmark models")
+    ap.add_argument("--optimizer", default="fused", choices=["fused", "foreach"],
+                    help="AdamW implementation (same update rule)")
     ap.add_argument("--storage", default="float32", choices=["float32", "bfloat16"],
                     help="storage type of the edge-sized interaction tensors (fp32 arithmetic)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
@@ -272,8 +274,11 @@ def main():
     params = make_params(args.layers, float(rmax.item()), args.lmax, args.storage)
     torch.manual_seed(0)
     model = EnergyEquivGNN(params).to(dev)
+    # AdamW(amsgrad) as the reference configures it (scripts/train_utils.py:39-43); the fused
+    # multi-tensor kernel is the same update in one launch per parameter group
     opt = torch.optim.AdamW(model.parameters(), lr=params.lr, betas=(params.beta1, 0.999),
-                            eps=params.epsilon, amsgrad=params.amsgrad, weight_decay=params.weight_decay)
+                            eps=params.epsilon, amsgrad=params.amsgrad, weight_decay=params.weight_decay,
+                            **({"fused": True} if args.optimizer == "fused" else {"foreach": True}))
     batch = collate(mine).to(dev)
     model.edge_graph(batch)     # CSR built once per batch (collate-time work)
     from gnn.parallel import FlatGradAllReduce, broadcast_parameters
