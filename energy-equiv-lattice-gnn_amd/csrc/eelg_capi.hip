@@ -418,8 +418,8 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
                      float* partial, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
-  if (chunk <= 0 || chunk % c->nb)
-    return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of %d", c->nb);
+  if (chunk <= 0 || chunk % c->nbc)
+    return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of %d", c->nbc);
   if (n_nodes <= 0) return 0;
   const int nch = (n_nodes + chunk - 1) / chunk;
   hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + c->wpb - 1) / c->wpb, nch, mul), dim3(64 * c->wpb), 0,

@@ -39,7 +39,8 @@ struct eelg_sc_cfg {
   eelg_sc_bwdc_fn bwd_coef;
   eelg_sc_cmajor_fn cmajor;      // input (coupling) layout
   eelg_sc_cmajor_fn cmajor_out;  // output layout
-  int nb;                        // nodes per fwd / grad-x workgroup and per coef-grad tile
+  int nb;                        // nodes per fwd / grad-x workgroup
+  int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -43,6 +43,9 @@ TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # 0.86): twice the VGPRs and LDS per workgroup halve the occupancy, the SGPR coefficient
 # operands need aligned pairs (s_mov per term), and dependent v_pk ops carry a wait state
 SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+# coefficient gradient: 64-node sub-tiles per staged LDS tile
+SC_COEF_SUB = int(os.environ.get("EELG_SC_COEF_SUB", "4"))
+SC_COEF_NOUNROLL = int(os.environ.get("EELG_SC_COEF_NOUNROLL", "0"))
 TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
 
 
@@ -751,7 +754,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 
     # ---------------- backward w.r.t. coefficients ----------------
     JG = 64 if PKN == 1 else 32               # terms per wave (packed: 2 nodes per accumulator)
-    NBC = 64 * PKN                            # nodes per staged tile
+    NSB = 64 * PKN                            # nodes per sub-tile (one lane each, or two packed)
+    NBC = NSB * SC_COEF_SUB                   # nodes per staged tile (one barrier pair)
     WPB = 8                                   # waves (term groups) per workgroup
     groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
     L.append(f"// coefficient gradient from channel-major x / g: {len(groups)} term groups of <= {JG};")
@@ -797,7 +801,14 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         out.append(f"        if (n0 + {NBC} < ne) {{")
         out += ["    " + ln for ln in issue(f"n0 + {NBC}")]
         out.append("        }")
-        out += body
+        if body:
+            # the wave sweeps the staged tile's sub-tiles with the same accumulators: more
+            # independent work per barrier pair
+            if SC_COEF_NOUNROLL:
+                out.append("#pragma unroll 1")
+            out.append(f"        for (int sb = 0; sb < {SC_COEF_SUB}; ++sb) {{")
+            out += body
+            out.append("        }")
         out.append("        __syncthreads();")
         out.append("      }")
         return out
@@ -819,9 +830,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         body = []
         # packed: a lane owns the adjacent nodes 2 * lane, 2 * lane + 1 of the tile (ds_read_b64)
         for a in sorted(need_x):
-            body.append(f"        const {FT} x{a} = *reinterpret_cast<const {FT}*>(&sx[{a * NBC} + {PKN} * lane]);")
+            body.append(f"        const {FT} x{a} = *reinterpret_cast<const {FT}*>(&sx[{a * NBC} + sb * {NSB} + {PKN} * lane]);")
         for q in sorted(need_g):
-            body.append(f"        const {FT} g{q} = *reinterpret_cast<const {FT}*>(&sg[{q * NBC} + {PKN} * lane]);")
+            body.append(f"        const {FT} g{q} = *reinterpret_cast<const {FT}*>(&sg[{q * NBC} + sb * {NSB} + {PKN} * lane]);")
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         cur = None
         for jj, t in enumerate(grp):
@@ -878,7 +889,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"    const int t = jg * {JG} + (lane >> {6 - k}); if (t < {nt}) dst[t] = {red}[0];")
     L.append("  }")
     L.append("}")
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -924,7 +935,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nb"]}}},')
+                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -138,7 +138,8 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
 int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
                    void* stream);
 /* Coefficient gradient from channel-major x and grad_out:
- * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk) (chunk % 64 == 0);
+ * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk) (chunk % 256 == 0 is
+ * always accepted; the generated tile may allow smaller multiples);
  * the caller sums over chunks (deterministic). */
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* grad_out_t, int n_nodes, int mul,
                      int chunk, float* partial, void* stream);
