@@ -75,7 +75,10 @@ __device__ __forceinline__ ChunkRef lin_chunk(const eelg_lin_slot& sl, int c) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void lin_fwd_kernel(const float* __restrict__ x, int x_row,
+#ifndef LIN_FWD_WPE
+#define LIN_FWD_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE))) void lin_fwd_kernel(const float* __restrict__ x, int x_row,
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ bias, int n_nodes,
                                                       float* __restrict__ y, int y_row,
@@ -249,7 +252,10 @@ __global__ __launch_bounds__(256) void lin_fwd_kernel(const float* __restrict__ 
 // chunks of floor(32/d) whole nodes round-robin, stage their X[row][u] / G[row][j] tiles
 // (node-contiguous 32*d-float runs) in wave-private LDS, reduce over rows with MFMA
 // (zero-padded to 32 rows), and the four accumulators are summed through LDS at the end.
-__global__ __launch_bounds__(256) void lin_bwdw_kernel(const float* __restrict__ x, int x_row,
+#ifndef LIN_BWDW_WPE
+#define LIN_BWDW_WPE 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_BWDW_WPE))) void lin_bwdw_kernel(const float* __restrict__ x, int x_row,
                                                        const float* __restrict__ g, int g_row,
                                                        int n_nodes, int nodes_per_slice,
                                                        float* __restrict__ partial, int w_total,
