@@ -37,6 +37,8 @@ MUL = 32
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
 TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
+TP_PIN_NEXT_LAST = int(os.environ.get("EELG_TP_PIN_NEXT_LAST", "1"))
+TP_FOLDW = int(os.environ.get("EELG_TP_FOLDW", "1"))   # fold the path weight into x or y
 TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # symmetric contraction: nodes per lane.  2 = packed-fp32 v_pk_* arithmetic on node pairs;
 # measured slower than 1 on MI355X (fwd 0.45 vs 0.35 ms, grad-x 0.76 vs 0.56, coef-grad 1.16 vs
@@ -168,6 +170,25 @@ def _emit_t(p: cg.TPPath, xname, yname, tname, L: List[str], ind: str):
     for k in range(d3):
         expr = " + ".join(terms_by_k[k]) if terms_by_k[k] else "0.0f"
         L.append(f"{ind}const float {tname}{k} = {expr};")
+
+
+def _emit_acc(p: cg.TPPath, xname, yname, aname, L: List[str], ind: str):
+    """a_k += sum_{ij} C_ijk x_i y_j for one path, straight into the accumulators (the path
+    weight already folded into x or y); cheaper of pair-products-first and M-first."""
+    nz = _path_cg(p)
+    pairs = sorted({(i, j) for (i, j, k), _ in nz})
+    iks = sorted({(i, k) for (i, j, k), _ in nz})
+    if len(pairs) <= len(iks):
+        for i, j in pairs:
+            L.append(f"{ind}const float z{i}_{j} = {xname(p, i)} * {yname(p, j)};")
+        for (i, j, k), c in nz:
+            L.append(f"{ind}{aname(k)} = fmaf({flit(c)}, z{i}_{j}, {aname(k)});")
+    else:
+        byik: Dict[Tuple[int, int], List[str]] = {}
+        for (i, j, k), c in nz:
+            byik.setdefault((i, k), []).append(f"{flit(c)} * {yname(p, j)}")
+        for (i, k), ts in byik.items():
+            L.append(f"{ind}{aname(k)} = fmaf({xname(p, i)}, {' + '.join(ts)}, {aname(k)});")
 
 
 _VT = {4: "eelg_f4u", 3: "eelg_f3u", 2: "eelg_f2u"}
@@ -310,16 +331,34 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             out.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
             out.extend("  " + ln for ln in load(np_, "e + 1", "s1", "e + 1 < eend"))
             cpin = pin(accs + [cp + v for v in cur] + ([] if TP_NOPIN_NEXT else [np_ + v for v in cur]))
+            # TP_PIN_NEXT_LAST: the in-flight next-edge registers are pinned only after the
+            # last path, so no earlier path boundary waits for the prefetch to land
+            cpin_mid = pin(accs + [cp + v for v in cur]) if TP_PIN_NEXT_LAST else cpin
             xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
             yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
             for p in grp:
+                d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
                 out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
                 out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
-                _emit_t(p, xn, yn, "t", out, "        ")
-                for k in range(2 * p.l3 + 1):
-                    out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+                fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y")) if TP_FOLDW else (0, "none")
+                if fold[1] == "none":
+                    _emit_t(p, xn, yn, "t", out, "        ")
+                    for k in range(d3):
+                        out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+                else:
+                    # fold the path weight into the shorter of x / y (d1 or d2 products instead
+                    # of d3 + 1) and accumulate the CG terms straight into the accumulators
+                    if fold[1] == "x":
+                        for i in range(d1):
+                            out.append(f"        const float xw{i} = {xn(p, i)} * wp;")
+                        xf, yf = (lambda p, i: f"xw{i}"), yn
+                    else:
+                        for j in range(d2):
+                            out.append(f"        const float yw{j} = {yn(p, j)} * wp;")
+                        xf, yf = xn, (lambda p, j: f"yw{j}")
+                    _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", out, "        ")
                 out.append("      }")
-                out.append("      " + cpin)
+                out.append("      " + (cpin if p is grp[-1] else cpin_mid))
             out.append("      s1 = s2; ++e; }")
             return out
         if TP_UNROLL2:

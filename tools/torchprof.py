@@ -27,7 +27,7 @@ def main():
     torch.manual_seed(0)
     model = EnergyEquivGNN(params).cuda()
     model.edge_graph(batch)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True, fused=True)
 
     def step():
         opt.zero_grad(set_to_none=True)
