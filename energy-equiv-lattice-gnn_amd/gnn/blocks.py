@@ -181,12 +181,19 @@ class TensorProductInteractionBlock(torch.nn.Module):
             self._cfg = _lib.tp_config_by_sig(self._sig)
         return self._cfg
 
+    def radial_weights(self, edge_feats: torch.Tensor) -> torch.Tensor:
+        """``conv_tp_weights(edge_feats)`` (``gnn/blocks.py:590``): the per-edge TP weights."""
+        return ops.radial_mlp(edge_feats, self.conv_tp_weights, self.storage_dtype)
+
     def forward(self, node_feats, edge_attrs, edge_feats, edge_index: EdgeIndex,
-                node_attrs: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, None]:
+                node_attrs: Optional[torch.Tensor] = None,
+                tp_weights: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, None]:
+        """``tp_weights``: ``radial_weights(edge_feats)`` computed ahead (possibly on another
+        stream, see ``GNN_Head``); computed here when not given."""
         csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
         idx, info = self._config()
         x = self.linear_up(node_feats)
-        w = ops.radial_mlp(edge_feats, self.conv_tp_weights, self.storage_dtype)
+        w = self.radial_weights(edge_feats) if tp_weights is None else tp_weights
         agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
         return self.linear(agg), None
 
@@ -206,7 +213,10 @@ class MACELayer(torch.nn.Module):
         self.product = EquivariantProductBlock(self.interaction.irreps_out, output_irreps,
                                                product_correlation, use_sc=False)
 
-    def forward(self, node_ft, edge_index: EdgeIndex, edge_sh, edge_scalars):
+    def forward(self, node_ft, edge_index: EdgeIndex, edge_sh, edge_scalars,
+                tp_weights: Optional[torch.Tensor] = None):
         csr, edge_sh, edge_scalars = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_scalars)
-        node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr)
+        if tp_weights is not None and not isinstance(edge_index, ops.EdgeCSR):
+            tp_weights = tp_weights[csr.perm]
+        node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr, tp_weights=tp_weights)
         return self.product(node_ft, sc)

@@ -15,6 +15,7 @@ Same constructor (``params`` Namespace), module tree, parameter names and
 """
 from __future__ import annotations
 
+import os
 from argparse import Namespace
 from typing import Any, Dict
 
@@ -37,6 +38,18 @@ def storage_dtype(params: Namespace) -> torch.dtype:
     if name not in table:
         raise ValueError(f"storage_dtype {name!r}: expected 'float32' or 'bfloat16'")
     return table[name]
+
+
+# radial MLPs of all layers on a side stream (EELG_OVERLAP_RADIAL=0 to run them in line)
+OVERLAP_RADIAL = os.environ.get("EELG_OVERLAP_RADIAL", "1") != "0"
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    idx = torch.device(device).index or 0
+    if idx not in _SIDE:
+        _SIDE[idx] = torch.cuda.Stream(device=device)
+    return _SIDE[idx]
 
 
 class GNN_Head(torch.nn.Module):  # noqa: N801
@@ -70,11 +83,41 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         self.cart_to_Mandel = Cart_4_to_Mandel()
         self.positive_layer = PositiveLayer(params)
 
+    def _radial_weights_ahead(self, edge_feats):
+        """Every layer's radial MLP depends only on the edge features, so all of them run up
+        front on a side stream and overlap the VALU-bound interaction / contraction kernels
+        of the main stream (their backward runs on that stream too: autograd replays a
+        backward op on its forward's stream and inserts the cross-stream waits).  Layer i
+        waits for its own weights only."""
+        if not (OVERLAP_RADIAL and edge_feats.is_cuda):
+            return [None] * self.num_interactions, [None] * self.num_interactions
+        main = torch.cuda.current_stream(edge_feats.device)
+        side = _side_stream(edge_feats.device)
+        side.wait_stream(main)
+        ws, evs = [], []
+        with torch.cuda.stream(side):
+            for layer in self.layers:
+                w = layer.interaction.radial_weights(edge_feats)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                ws.append(w)
+                evs.append(ev)
+        for w in ws:
+            w.record_stream(main)        # allocator: w is also used on the main stream
+        return ws, evs
+
     def forward(self, edge_index, node_ft, edge_sh, edge_feats, batch_idx, num_graphs: int):
         csr, edge_sh, edge_feats = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_feats)
-        node_ft = self.layers[0](node_ft, csr, edge_sh, edge_feats)
+        ws, evs = self._radial_weights_ahead(edge_feats)
+
+        def run(i, h):
+            if evs[i] is not None:
+                torch.cuda.current_stream(h.device).wait_event(evs[i])
+            return self.layers[i](h, csr, edge_sh, edge_feats, tp_weights=ws[i])
+
+        node_ft = run(0, node_ft)
         for i in range(1, self.num_interactions):
-            node_ft = node_ft + self.layers[i](node_ft, csr, edge_sh, edge_feats)
+            node_ft = node_ft + run(i, node_ft)
         out = self.nonlin_readout(node_ft)
         graph_ft = ops.graph_pool(out, batch_idx, num_graphs, self.global_reduction)
         stiff = self.sph_to_cart(self.linear(graph_ft))
