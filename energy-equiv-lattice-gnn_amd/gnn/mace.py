@@ -91,4 +91,16 @@ class SymmetricContraction(torch.nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idx, info = self._config()
-        return ops.symmetric_contraction(x, self.coefficients(), idx, info, self.mul)
+        side = ops.side_stream(x.device, 1) if (ops.OVERLAP and x.is_cuda) else None
+        if side is None:
+            return ops.symmetric_contraction(x, self.coefficients(), idx, info, self.mul)
+        # the coefficient chain (weight matrix -> U_sym SpMM) runs on the side stream, so its
+        # backward -- and the coefficient-gradient kernel launched there by the contraction's
+        # backward -- overlaps the rest of the backward on the main stream
+        main = torch.cuda.current_stream(x.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            coef = self.coefficients()
+        main.wait_stream(side)
+        coef.record_stream(main)
+        return ops.symmetric_contraction(x, coef, idx, info, self.mul, side=side)

@@ -15,7 +15,6 @@ Same constructor (``params`` Namespace), module tree, parameter names and
 """
 from __future__ import annotations
 
-import os
 from argparse import Namespace
 from typing import Any, Dict
 
@@ -38,18 +37,6 @@ def storage_dtype(params: Namespace) -> torch.dtype:
     if name not in table:
         raise ValueError(f"storage_dtype {name!r}: expected 'float32' or 'bfloat16'")
     return table[name]
-
-
-# radial MLPs of all layers on a side stream (EELG_OVERLAP_RADIAL=0 to run them in line)
-OVERLAP_RADIAL = os.environ.get("EELG_OVERLAP_RADIAL", "1") != "0"
-_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    idx = torch.device(device).index or 0
-    if idx not in _SIDE:
-        _SIDE[idx] = torch.cuda.Stream(device=device)
-    return _SIDE[idx]
 
 
 class GNN_Head(torch.nn.Module):  # noqa: N801
@@ -89,10 +76,10 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         of the main stream (their backward runs on that stream too: autograd replays a
         backward op on its forward's stream and inserts the cross-stream waits).  Layer i
         waits for its own weights only."""
-        if not (OVERLAP_RADIAL and edge_feats.is_cuda):
+        if not (ops.OVERLAP and edge_feats.is_cuda):
             return [None] * self.num_interactions, [None] * self.num_interactions
         main = torch.cuda.current_stream(edge_feats.device)
-        side = _side_stream(edge_feats.device)
+        side = ops.side_stream(edge_feats.device)
         side.wait_stream(main)
         ws, evs = [], []
         with torch.cuda.stream(side):

@@ -5,6 +5,7 @@ There is no eager/CPU fallback: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -46,6 +47,20 @@ class KernelTimer:
 
 
 TIMER = KernelTimer()
+
+# side-stream overlap of independent work (radial MLPs, symmetric-contraction coefficient
+# chain and its gradient); EELG_OVERLAP=0 runs everything in line on the current stream
+OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
+_SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
+
+
+def side_stream(device, which: int = 0) -> "torch.cuda.Stream":
+    """Side stream ``which`` of ``device``: 0 = radial MLPs, 1 = contraction coefficients."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if (idx, which) not in _SIDE:
+        _SIDE[(idx, which)] = torch.cuda.Stream(device=torch.device("cuda", idx))
+    return _SIDE[(idx, which)]
 
 
 def _require_device(*ts):
@@ -262,7 +277,7 @@ def tp_interaction(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_n
 # ---------------------------------------------------------------------------
 class _SymCon(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int):
+    def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int, side=None):
         x, coef = _f32(x), _f32(coef)
         n = x.shape[0]
         if x.shape[1] != info["x_row"] or coef.shape != (mul, info["nterms"]):
@@ -274,7 +289,7 @@ class _SymCon(torch.autograd.Function):
                                    _lib.stream()), "sc_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, coef)
-        ctx.cfg, ctx.info, ctx.mul = cfg, info, mul
+        ctx.cfg, ctx.info, ctx.mul, ctx.side = cfg, info, mul, side
         return out
 
     @staticmethod
@@ -309,17 +324,35 @@ class _SymCon(torch.autograd.Function):
             chunk = max(256, min(4096, (n // 16 + 255) // 256 * 256))   # a multiple of the tile
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
-            tok = TIMER.start("sc_bwd_coef")
-            _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul, chunk,
-                                            _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
-            TIMER.stop(tok)
-            gcoef = part.sum(0)
-        return gx, gcoef, None, None, None
+            side = ctx.side
+            if side is not None:
+                # the coefficient gradient runs on the side stream, where its consumer (the
+                # coefficient chain's backward) runs too; the main stream goes on meanwhile
+                side.wait_stream(torch.cuda.current_stream(x.device))
+                for t in (xt, gt, part):
+                    t.record_stream(side)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                tok = TIMER.start("sc_bwd_coef")
+                _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul,
+                                                chunk, _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
+                TIMER.stop(tok)
+                gcoef = part.sum(0)
+        return gx, gcoef, None, None, None, None
 
 
-def symmetric_contraction(x, coef, cfg: int, info: Dict[str, int], mul: int):
+def symmetric_contraction(x, coef, cfg: int, info: Dict[str, int], mul: int, side=None):
+    """``side``: the stream ``coef`` was produced on (its backward's stream); the
+    coefficient gradient is then computed there."""
     _require_device(x, coef)
-    return _SymCon.apply(x, coef, cfg, info, mul)
+    return _SymCon.apply(x, coef, cfg, info, mul, side)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 # ---------------------------------------------------------------------------
