@@ -21,22 +21,47 @@ from . import cg
 from .irreps import Irreps
 
 
+class _OnStream(torch.autograd.Function):
+    """Identity (a view) applied while ``stream`` is current, so that autograd runs its
+    backward -- and the gradient accumulation of the parameter behind it -- on ``stream``."""
+
+    @staticmethod
+    def forward(ctx, t, stream):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
 class _IrrepsLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, lin: "Linear"):
+    def forward(ctx, x, weight, bias, lin: "Linear", side=None):
         ctx.save_for_backward(x, weight)
-        ctx.lin = lin
+        ctx.lin, ctx.side = lin, side
         return lin._fwd(x, weight, bias)
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
-        lin = ctx.lin
+        lin, side = ctx.lin, ctx.side
         gy = gy.contiguous()
         gx = lin._bwd_x(gy, weight) if ctx.needs_input_grad[0] else None
-        gw = lin._bwd_w(x, gy) if ctx.needs_input_grad[1] else None
-        gb = lin._bwd_bias(gy) if ctx.needs_input_grad[2] else None
-        return gx, gw, gb, None
+        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        if side is None or not (want_w or want_b):
+            gw = lin._bwd_w(x, gy) if want_w else None
+            gb = lin._bwd_bias(gy) if want_b else None
+            return gx, gw, gb, None, None
+        # weight / bias gradients on the side stream the parameters' views were made on:
+        # their consumers (the views' backward, the accumulation) run there as well, and
+        # the main stream carries on with grad-x
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        x.record_stream(side)
+        gy.record_stream(side)
+        with torch.cuda.stream(side):
+            gw = lin._bwd_w(x, gy) if want_w else None
+            gb = lin._bwd_bias(gy) if want_b else None
+        return gx, gw, gb, None, None
 
 
 class Linear(torch.nn.Module):
@@ -174,7 +199,16 @@ class Linear(torch.nn.Module):
         _require_device(x)
         if x.shape[-1] != self.irreps_in.dim:
             raise ValueError(f"Linear expects [..., {self.irreps_in.dim}], got {tuple(x.shape)}")
-        return _IrrepsLinearFn.apply(_f32(x), self.weight, self.bias, self)
+        from . import ops
+        weight, bias = self.weight, self.bias
+        side = None
+        if ops.OVERLAP and x.is_cuda and torch.is_grad_enabled() and weight.requires_grad:
+            side = ops.side_stream(x.device, 2)
+            with torch.cuda.stream(side):
+                weight = _OnStream.apply(weight, side)
+                if bias is not None:
+                    bias = _OnStream.apply(bias, side)
+        return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side)
 
 
 class Gate(torch.nn.Module):
