@@ -15,6 +15,7 @@ Same constructor (``params`` Namespace), module tree, parameter names and
 """
 from __future__ import annotations
 
+import os
 from argparse import Namespace
 from typing import Any, Dict
 
@@ -37,6 +38,10 @@ def storage_dtype(params: Namespace) -> torch.dtype:
     if name not in table:
         raise ValueError(f"storage_dtype {name!r}: expected 'float32' or 'bfloat16'")
     return table[name]
+
+
+# every layer's radial MLP done before layer 1 starts (they overlap layer 0 only)
+RADIAL_AHEAD_OF_LAYER1 = os.environ.get("EELG_RADIAL_BEFORE_L1", "1") != "0"
 
 
 class GNN_Head(torch.nn.Module):  # noqa: N801
@@ -103,6 +108,9 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
             return self.layers[i](h, csr, edge_sh, edge_feats, tp_weights=ws[i])
 
         node_ft = run(0, node_ft)
+        if RADIAL_AHEAD_OF_LAYER1 and evs[-1] is not None:
+            # the later layers' interaction kernels run without the MLP GEMMs beside them
+            torch.cuda.current_stream(node_ft.device).wait_event(evs[-1])
         for i in range(1, self.num_interactions):
             node_ft = node_ft + run(i, node_ft)
         out = self.nonlin_readout(node_ft)
