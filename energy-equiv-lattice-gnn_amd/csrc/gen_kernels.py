@@ -38,6 +38,8 @@ TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
 TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
 TP_PIN_NEXT_LAST = int(os.environ.get("EELG_TP_PIN_NEXT_LAST", "1"))
+TP_PK2 = int(os.environ.get("EELG_TP_PK2", "0"))        # packed channel-pair forward
+TP_PK2_MAXACC = int(os.environ.get("EELG_TP_PK2_MAXACC", "16"))
 TP_FOLDW = int(os.environ.get("EELG_TP_FOLDW", "1"))   # fold the path weight into x or y
 TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # symmetric contraction: nodes per lane.  2 = packed-fp32 v_pk_* arithmetic on node pairs;
@@ -232,6 +234,105 @@ def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
     return out
 
 
+def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) -> List[str]:
+    """Packed-fp32 forward (TP_PK2): a lane owns the channel PAIR (c0, c0 + 1) of one
+    receiver stream, 16 lanes per stream, 4 streams per wave.  The CG contractions run in
+    M-first form: M_ik = sum_j C_ijk y_j is edge-only data (scalar VALU with literal CG
+    constants, shared by the two channels) and a_k += (w x_i) M_ik is one v_pk_fma_f32 for
+    both channels; the path weight is folded into the x pair."""
+    L: List[str] = []
+    ng = len(groups)
+    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append("  const int lane = threadIdx.x & 63;")
+    L.append("  const int c0 = (lane & 15) * 2;")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
+    L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4)) * {TP_NPH};")
+    L.append("  if (n0 >= n_nodes) return;")
+    L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
+    L.append("  switch (grp) {")
+    for gi, grp in enumerate(groups):
+        L.append(f"  case {gi}: {{")
+        need_l1 = sorted({p.l1 for p in grp})
+        need_l2 = sorted({p.l2 for p in grp})
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        L.append("    eelg_f2 " + ", ".join(f"{a} = {{0.0f, 0.0f}}" for a in accs) + ";")
+        curf = ([f"xr{l}_{i}" for l in need_l1 for i in range(2 * (2 * l + 1))]
+                + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)])
+        curv = [f"w{p.slot}" for p in grp]
+
+        def load(pref, ev, sv, guard):
+            out = [f"    {{ const bool ok = {guard};",
+                   f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
+                   f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
+                   f"      const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + c0;"]
+            for l in need_l1:
+                d = 2 * l + 1
+                # channels c0, c0 + 1 of block l: 2d consecutive floats
+                out += ["      " + ln for ln in vec_load([f"{pref}xr{l}_{i}" for i in range(2 * d)], "xs",
+                                                          f"{node_off[l]} + c0 * {d}")]
+            out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
+            for p in grp:
+                if bf:
+                    out.append(f"      {{ const unsigned v_ = *reinterpret_cast<const unsigned*>(we + {p.slot * MUL}); "
+                               f"{pref}w{p.slot} = eelg_f2{{__uint_as_float(v_ << 16), __uint_as_float(v_ & 0xffff0000u)}}; }}")
+                else:
+                    out.append(f"      {pref}w{p.slot} = *reinterpret_cast<const eelg_f2*>(we + {p.slot * MUL});")
+            out.append("    }")
+            return out
+        L.append("    int e = rowptr[n0];")
+        L.append("    const int eend = rowptr[n1];")
+        L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
+        L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
+        L.append("    float " + ", ".join(curf) + ";")
+        L.append("    eelg_f2 " + ", ".join(curv) + ";")
+        L += load("", "e", "(e < eend ? sender[e] : 0)", "e < eend")
+        cur = curf + curv
+        L.append("    for (;;) {")
+        L.append("      float " + ", ".join("n" + v for v in curf) + ";")
+        L.append("      eelg_f2 " + ", ".join("n" + v for v in curv) + ";")
+        L.append("      while (node < n1 && nend == e) {")
+        L.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            vals = [f"a{p.slot}_{k}.x" for k in range(d3)] + [f"a{p.slot}_{k}.y" for k in range(d3)]
+            L.extend("        " + ln for ln in vec_store(vals, "o", f"{p.out_off} + c0 * {d3}"))
+        L.append("        " + " ".join(f"{a} = eelg_f2{{0.0f, 0.0f}};" for a in accs))
+        L.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
+        L.append("      }")
+        L.append("      if (e >= eend) break;")
+        L.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
+        L.extend("  " + ln for ln in load("n", "e + 1", "s1", "e + 1 < eend"))
+        cpin_mid = pin(accs + cur)
+        cpin_last = pin(accs + cur + ["n" + v for v in cur])
+        for p in grp:
+            d1 = 2 * p.l1 + 1
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const eelg_f2 wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
+            for i in range(d1):
+                L.append(f"        const eelg_f2 xw{i} = eelg_f2{{xr{p.l1}_{i}, xr{p.l1}_{d1 + i}}} * wp;")
+            nz = _path_cg(p)
+            byik: Dict[Tuple[int, int], List[str]] = {}
+            for (i, j, k), c in nz:
+                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
+            for (i, k), ts in byik.items():
+                L.append(f"        {{ const float m = {' + '.join(ts)}; "
+                         f"a{p.slot}_{k} = eelg_fma2(xw{i}, eelg_f2{{m, m}}, a{p.slot}_{k}); }}")
+            L.append("      }")
+            L.append("      " + (cpin_last if p is grp[-1] else cpin_mid))
+        L.append("      s1 = s2; ++e; }")
+        L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
+        L.append("    }")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -248,7 +349,9 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     wn = sum(p.mul for p in paths)
     for p in paths:
         assert p.mul == MUL
-    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), TP_MAXACC)
+    pk2 = TP_PK2 and [ir.l for _, ir in node] != [0]
+    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)),
+                          TP_PK2_MAXACC if pk2 else TP_MAXACC)
     node_ls = [ir.l for _, ir in node]
     node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
     L: List[str] = []
@@ -267,8 +370,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
+    if TP_PK2 and node_ls != [0]:
+        L += emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off)
+        fwd_done = True
+    else:
+        fwd_done = False
     wpe = f" __attribute__((amdgpu_waves_per_eu({TP_WPE})))" if TP_WPE else ""
-    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}{sfx}(")
+    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}{sfx}{'_unused' if fwd_done else ''}(")
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
@@ -462,7 +570,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  }")
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
-                npaths=len(paths), nph=TP_NPH,
+                npaths=len(paths), nph=2 * TP_NPH if pk2 else TP_NPH,
                 sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
