@@ -302,3 +302,31 @@ def test_symcon_grad_x_writes_channel_major_copies(n):
     torch.cuda.synchronize()
     assert torch.equal(gx0, gx1)
     assert torch.equal(xt0, xt1) and torch.equal(gt0, gt1)
+
+
+def test_stream_overlap_matches_in_line_bitwise():
+    """The side-stream overlap (radial MLPs, contraction coefficients and their gradients,
+    linear weight gradients) changes only where kernels run, not what they compute: the
+    stiffness and every parameter gradient are bit-identical to the in-line run."""
+    from gnn import ops
+    from gnn.model import EnergyEquivGNN
+    from gnn.train import stiffness_loss
+    b, bd, csr, rmax = _setup()
+    p = params(4, max_edge_radius=rmax)
+    torch.manual_seed(0)
+    m = EnergyEquivGNN(p).to(DEV)
+    saved = ops.OVERLAP
+    outs = []
+    try:
+        for flag in (False, True):
+            ops.OVERLAP = flag
+            m.zero_grad(set_to_none=True)
+            c = m(bd)["stiffness"]
+            stiffness_loss(c, bd.stiffness).backward()
+            torch.cuda.synchronize()
+            outs.append((c.detach().clone(), [q.grad.clone() for q in m.parameters()]))
+    finally:
+        ops.OVERLAP = saved
+    assert torch.equal(outs[0][0], outs[1][0])
+    for g0, g1 in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(g0, g1)
