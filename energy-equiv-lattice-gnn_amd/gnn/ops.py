@@ -51,6 +51,7 @@ TIMER = KernelTimer()
 # side-stream overlap of independent work (radial MLPs, symmetric-contraction coefficient
 # chain and its gradient); EELG_OVERLAP=0 runs everything in line on the current stream
 OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
+SC_CMAJOR_ON_SIDE = os.environ.get("EELG_SC_CMAJOR_SIDE", "0") != "0"   # measured equal; fused keeps fewer bytes
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
@@ -303,18 +304,32 @@ class _SymCon(torch.autograd.Function):
         if want_c:
             xt = torch.empty(ctx.mul * ctx.info["D"], n, device=x.device, dtype=torch.float32)
             gt = torch.empty(ctx.mul * ctx.info["Dout"], n, device=x.device, dtype=torch.float32)
+        # with a side stream, the channel-major transposes move there with the coef-grad
+        # (off the main chain); in line, grad-x writes them from the tiles it stages anyway
+        cm_side = want_c and ctx.side is not None and SC_CMAJOR_ON_SIDE
+        if cm_side:
+            # launched before grad-x: the transposes need only x and grad_out, and run beside it
+            side = ctx.side
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            for t in (x, g, xt, gt):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
+                                              _lib.stream()), "sc_cmajor")
+                _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
+                                              _lib.stream()), "sc_cmajor")
         if want_x:
-            # grad-x; its staged tiles also give the channel-major operands of the coef-grad
             gx = torch.empty_like(x)
             tok = TIMER.start("sc_bwd_x")
+            fuse = want_c and not cm_side
             _lib.check(lib.eelg_sc_bwd_x_cm(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
                                             ctx.mul, _lib.ptr(gx),
-                                            _lib.ptr(xt) if want_c else None,
-                                            _lib.ptr(gt) if want_c else None, _lib.stream()),
+                                            _lib.ptr(xt) if fuse else None,
+                                            _lib.ptr(gt) if fuse else None, _lib.stream()),
                        "sc_bwd_x")
             TIMER.stop(tok)
         if want_c:
-            if not want_x:
+            if not (want_x or cm_side):
                 tok = TIMER.start("sc_cmajor")
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
                                               _lib.stream()), "sc_cmajor")
@@ -328,7 +343,8 @@ class _SymCon(torch.autograd.Function):
             if side is not None:
                 # the coefficient gradient runs on the side stream, where its consumer (the
                 # coefficient chain's backward) runs too; the main stream goes on meanwhile
-                side.wait_stream(torch.cuda.current_stream(x.device))
+                if not cm_side:
+                    side.wait_stream(torch.cuda.current_stream(x.device))
                 for t in (xt, gt, part):
                     t.record_stream(side)
             with torch.cuda.stream(side) if side is not None else _nullctx():
