@@ -296,7 +296,7 @@ int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const 
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_edges <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd, dim3((n_edges + 7) / 8, c->nbgroups), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, w, sender, receiver, n_edges, grad_agg, inv_norm,
                      grad_w, gxe);
   return check_launch("tp_bwd");
@@ -308,7 +308,7 @@ int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_edges <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 7) / 8, c->nbgroups), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sender,
                      receiver, n_edges, grad_agg, inv_norm, static_cast<unsigned short*>(grad_w),
                      static_cast<unsigned short*>(gxe));

@@ -22,7 +22,8 @@ typedef void (*eelg_sc_cmajor_fn)(const float*, int, float*);
 struct eelg_tp_cfg {
   const char* name;
   int din, dmid, wn, nsh, ngroups, npaths, lmax, nbgroups;
-  int nph;  // tp_fwd: receivers per half-wave
+  int nph;   // tp_fwd: receivers per half-wave
+  int beph;  // tp_bwd: edges per half-wave
   uint64_t sig;
   eelg_tp_fwd_fn fwd;
   eelg_tp_bwd_fn bwd;

@@ -38,6 +38,7 @@ TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
 TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
 TP_PIN_NEXT_LAST = int(os.environ.get("EELG_TP_PIN_NEXT_LAST", "1"))
+TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 TP_PK2 = int(os.environ.get("EELG_TP_PK2", "0"))        # packed channel-pair forward
 TP_PK2_MAXACC = int(os.environ.get("EELG_TP_PK2_MAXACC", "16"))
 TP_FOLDW = int(os.environ.get("EELG_TP_FOLDW", "1"))   # fold the path weight into x or y
@@ -499,78 +500,105 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe) {{")
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
-    L.append("  const int e = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
-    L.append("  if (e >= n_edges) return;")
-    L.append("  const float* __restrict__ xs = x + (size_t)sender[e] * " + str(din) + ";")
-    L.append("  const float* __restrict__ ye = sh + (size_t)e * " + str(nshp) + ";")
-    L.append(f"  const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
-    L.append(f"  {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
-    L.append("  const float* __restrict__ ge = gagg + (size_t)receiver[e] * " + str(dmid) + ";")
-    L.append(f"  {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
+    # a half-wave streams TP_BWD_EPH consecutive edges: while the last path of edge e
+    # computes, edge e+1's x / SH rows and first path's grad_agg slice and weight are in
+    # flight (its sender / receiver indices were loaded when edge e started)
+    EPH = TP_BWD_EPH
+    L.append(f"  const int e0 = ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {EPH};")
+    L.append("  if (e0 >= n_edges) return;")
+    L.append(f"  const int e1 = min(e0 + {EPH}, n_edges);")
     L.append("  switch (blockIdx.y) {")
     for gi, grp in enumerate(bgroups):
         l = grp[0].l1
         d = 2 * l + 1
-        L.append(f"  case {gi}: {{ // input block l1 = {l}")
-        L.append("    float " + ", ".join(f"x{l}_{i}" for i in range(d)) + ";")
-        L += ["    " + ln for ln in vec_load([f"x{l}_{i}" for i in range(d)], "xs", f"{node_off[l]} + u * {d}")]
-        for i in range(d):
-            L.append(f"    float gx{l}_{i} = 0.0f;")
         l2s = sorted({p.l2 for p in grp})
-        L.append("    float " + ", ".join(f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)) + ";")
-        L += ["    " + ln for ln in sh_load(l2s, "", "ye")]
-        base_pin = ([f"x{l}_{i}" for i in range(d)] + [f"gx{l}_{i}" for i in range(d)]
-                    + [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)])
+        xs_ = [f"x{l}_{i}" for i in range(d)]
+        ys_ = [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)]
+        p0 = grp[0]
+        g0_ = [f"g{p0.slot}_{k}" for k in range(2 * p0.l3 + 1)] + [f"w{p0.slot}"]
+        L.append(f"  case {gi}: {{ // input block l1 = {l}")
+
+        def edge_loads(pref, sv, rv, ev):
+            """x / SH rows of an edge and its first path's grad_agg slice + weight"""
+            out = [f"    {{ const float* __restrict__ xs = x + (size_t){sv} * {din};",
+                   f"      const float* __restrict__ ye = sh + (size_t){ev} * {nshp};",
+                   f"      const float* __restrict__ ge = gagg + (size_t){rv} * {dmid};",
+                   f"      const {WT}* __restrict__ we = w + (size_t){ev} * {wn} + u;"]
+            out += ["      " + ln for ln in vec_load([pref + v for v in xs_], "xs", f"{node_off[l]} + u * {d}")]
+            out += ["      " + ln for ln in sh_load(l2s, pref, "ye")]
+            d3 = 2 * p0.l3 + 1
+            out += ["      " + ln for ln in vec_load([f"{pref}g{p0.slot}_{k}" for k in range(d3)], "ge",
+                                                      f"{p0.out_off} + u * {d3}")]
+            out.append(f"      {pref}w{p0.slot} = {ld_w(f'we[{p0.slot * MUL}]')};")
+            out.append("    }")
+            return out
+        L.append("    float " + ", ".join(xs_ + ys_ + g0_) + ";")
+        L.append("    int rcur = receiver[e0];")
+        L += edge_loads("", "sender[e0]", "rcur", "e0")
+        L.append("    for (int e = e0; e < e1; ++e) {")
+        L.append("      const bool more = e + 1 < e1;")
+        L.append("      const int sn = more ? sender[e + 1] : 0, rn = more ? receiver[e + 1] : 0;")
+        L.append("      const int en = more ? e + 1 : e;")
+        L.append("      const float* __restrict__ ge = gagg + (size_t)rcur * " + str(dmid) + ";")
+        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
+        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
+        L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
+        for i in range(d):
+            L.append(f"      float gx{l}_{i} = 0.0f;")
+        L.append("      float " + ", ".join("n" + v for v in xs_ + ys_ + g0_) + ";")
+        base_pin = xs_ + [f"gx{l}_{i}" for i in range(d)] + ys_
 
         def pref(p):
             """issue the loads one path needs (its grad_agg slot row and weight)"""
             d3 = 2 * p.l3 + 1
-            out = ["    float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
-            out += ["    " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
-                                                  f"{p.out_off} + u * {d3}")]
-            out.append(f"    float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
+            out = ["      float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
+            out += ["      " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
+                                                    f"{p.out_off} + u * {d3}")]
+            out.append(f"      float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
-        first, _ = pref(grp[0])
-        L += first
         for pi, p in enumerate(grp):
             d3 = 2 * p.l3 + 1
             d1 = 2 * p.l1 + 1
-            nxt_regs = []
             if pi + 1 < len(grp):            # next path's loads in flight during this one
                 code, nxt_regs = pref(grp[pi + 1])
                 L += code
-            L.append(f"    {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-            L.append(f"      const float cp = {flit(p.coef)} * inv_norm;")
+            else:                            # next edge's loads in flight during the last path
+                L += ["  " + ln for ln in edge_loads("n", "sn", "rn", "en")]
+                nxt_regs = ["n" + v for v in xs_ + ys_ + g0_]
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
             nz = _path_cg(p)
             byik: Dict[Tuple[int, int], List[str]] = {}
             for (i, j, k), c in nz:
                 byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
             for (i, k), ts in byik.items():
-                L.append(f"      const float m{i}_{k} = {' + '.join(ts)};")
+                L.append(f"        const float m{i}_{k} = {' + '.join(ts)};")
             gterms = []
             for k in range(d3):
                 ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
                 if ts:
                     gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
             gexpr = " + ".join(gterms) if gterms else "0.0f"
-            L.append(f"      gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
-            L.append(f"      const float hw = cp * w{p.slot};")
+            L.append(f"        gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
+            L.append(f"        const float hw = cp * w{p.slot};")
             for i in range(d1):
                 ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
                 if ts:
-                    L.append(f"      gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
-            L.append("    }")
-            L.append("    " + pin(base_pin + nxt_regs))
+                    L.append(f"        gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
+            L.append("      }")
+            L.append("      " + pin(base_pin + nxt_regs))
         if bf:
-            L += [f"    gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
+            L += [f"      gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
         else:
-            L += ["    " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
+            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
+        L.append("      " + " ".join(f"{v} = n{v};" for v in xs_ + ys_ + g0_) + " rcur = rn;")
+        L.append("    }")
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
-                npaths=len(paths), nph=2 * TP_NPH if pk2 else TP_NPH,
+                npaths=len(paths), nph=2 * TP_NPH if pk2 else TP_NPH, beph=TP_BWD_EPH,
                 sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
@@ -1075,7 +1103,7 @@ def main(outdir: str) -> None:
     for name, i in tp_table:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
-                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
+                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
                      f'tp_fwd_{name}_bw, tp_bwd_{name}_bw}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
