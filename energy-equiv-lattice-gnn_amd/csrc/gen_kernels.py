@@ -536,16 +536,18 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
         L.append("    int rcur = receiver[e0];")
         L += edge_loads("", "sender[e0]", "rcur", "e0")
         L.append("    for (int e = e0; e < e1; ++e) {")
-        L.append("      const bool more = e + 1 < e1;")
-        L.append("      const int sn = more ? sender[e + 1] : 0, rn = more ? receiver[e + 1] : 0;")
-        L.append("      const int en = more ? e + 1 : e;")
+        if EPH > 1:
+            L.append("      const bool more = e + 1 < e1;")
+            L.append("      const int sn = more ? sender[e + 1] : 0, rn = more ? receiver[e + 1] : 0;")
+            L.append("      const int en = more ? e + 1 : e;")
         L.append("      const float* __restrict__ ge = gagg + (size_t)rcur * " + str(dmid) + ";")
         L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
         L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
         L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
         for i in range(d):
             L.append(f"      float gx{l}_{i} = 0.0f;")
-        L.append("      float " + ", ".join("n" + v for v in xs_ + ys_ + g0_) + ";")
+        if EPH > 1:
+            L.append("      float " + ", ".join("n" + v for v in xs_ + ys_ + g0_) + ";")
         base_pin = xs_ + [f"gx{l}_{i}" for i in range(d)] + ys_
 
         def pref(p):
@@ -562,9 +564,11 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             if pi + 1 < len(grp):            # next path's loads in flight during this one
                 code, nxt_regs = pref(grp[pi + 1])
                 L += code
-            else:                            # next edge's loads in flight during the last path
+            elif EPH > 1:                    # next edge's loads in flight during the last path
                 L += ["  " + ln for ln in edge_loads("n", "sn", "rn", "en")]
                 nxt_regs = ["n" + v for v in xs_ + ys_ + g0_]
+            else:
+                nxt_regs = []
             L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
             L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
             nz = _path_cg(p)
@@ -591,7 +595,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             L += [f"      gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
         else:
             L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
-        L.append("      " + " ".join(f"{v} = n{v};" for v in xs_ + ys_ + g0_) + " rcur = rn;")
+        if EPH > 1:
+            L.append("      " + " ".join(f"{v} = n{v};" for v in xs_ + ys_ + g0_) + " rcur = rn;")
         L.append("    }")
         L.append("    break; }")
     L.append("  default: break;")
