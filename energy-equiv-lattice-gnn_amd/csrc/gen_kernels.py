@@ -40,6 +40,7 @@ TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
 TP_PIN_NEXT_LAST = int(os.environ.get("EELG_TP_PIN_NEXT_LAST", "1"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 TP_PK2 = int(os.environ.get("EELG_TP_PK2", "0"))        # packed channel-pair forward
+TP_PK2_YNOW = int(os.environ.get("EELG_TP_PK2_YNOW", "0"))
 TP_PK2_MAXACC = int(os.environ.get("EELG_TP_PK2_MAXACC", "16"))
 TP_FOLDW = int(os.environ.get("EELG_TP_FOLDW", "1"))   # fold the path weight into x or y
 TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
@@ -243,7 +244,8 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
     both channels; the path weight is folded into the x pair."""
     L: List[str] = []
     ng = len(groups)
-    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}{sfx}(")
+    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_WPE})))" if TP_WPE else ""
+    L.append(f"__global__ __launch_bounds__(256){wpe} void tp_fwd_{name}{sfx}(")
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
@@ -261,8 +263,9 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
         need_l2 = sorted({p.l2 for p in grp})
         accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
         L.append("    eelg_f2 " + ", ".join(f"{a} = {{0.0f, 0.0f}}" for a in accs) + ";")
+        ysh = [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
         curf = ([f"xr{l}_{i}" for l in need_l1 for i in range(2 * (2 * l + 1))]
-                + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)])
+                + ([] if TP_PK2_YNOW else ysh))
         curv = [f"w{p.slot}" for p in grp]
 
         def load(pref, ev, sv, guard):
@@ -275,7 +278,8 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
                 # channels c0, c0 + 1 of block l: 2d consecutive floats
                 out += ["      " + ln for ln in vec_load([f"{pref}xr{l}_{i}" for i in range(2 * d)], "xs",
                                                           f"{node_off[l]} + c0 * {d}")]
-            out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
+            if not TP_PK2_YNOW:
+                out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
             for p in grp:
                 if bf:
                     out.append(f"      {{ const unsigned v_ = *reinterpret_cast<const unsigned*>(we + {p.slot * MUL}); "
@@ -306,6 +310,12 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
         L.append("      }")
         L.append("      if (e >= eend) break;")
         L.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
+        if TP_PK2_YNOW:
+            # this edge's SH row, loaded now (no prefetch registers for it)
+            L.append("        float " + ", ".join(ysh) + ";")
+            L.append(f"        {{ const float* __restrict__ ye = sh + (size_t)e * {nshp};")
+            L += ["          " + ln for ln in sh_load(need_l2, "", "ye")]
+            L.append("        }")
         L.extend("  " + ln for ln in load("n", "e + 1", "s1", "e + 1 < eend"))
         cpin_mid = pin(accs + cur)
         cpin_last = pin(accs + cur + ["n" + v for v in cur])
