@@ -207,9 +207,11 @@ class _SegmentMean(torch.autograd.Function):
 
 def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
     _require_device(src)
-    cnt = torch.bincount(batch, minlength=num_graphs)
-    ptr = torch.zeros(num_graphs + 1, dtype=torch.int32, device=src.device)
-    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    # ``batch`` is sorted (PyG collation), so the segment bounds are a searchsorted: no
+    # device -> host sync (bincount sizes its output from the data and would stall the host)
+    bounds = torch.arange(num_graphs + 1, device=batch.device, dtype=batch.dtype)
+    ptr = torch.searchsorted(batch, bounds).to(torch.int32)
+    cnt = (ptr[1:] - ptr[:-1]).to(torch.int64)
     if reduce == "mean":
         inv = 1.0 / cnt.clamp_min(1).to(torch.float32)
     elif reduce == "sum":
