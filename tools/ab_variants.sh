@@ -1,3 +1,7 @@
+#!/bin/bash
+# A/B of kernel variants built by tools/build_variant.sh (variants/libeelg_<tag>.so, loaded via
+# EELG_LIB; "main" = the in-tree library): TP parity tests, then tools/kbench.py timings.
+# usage (GPU box): bash tools/ab_variants.sh main <tag> [<tag> ...]
 set -e
 mkdir -p gpurun_out/var
 for v in "$@"; do

@@ -1,3 +1,8 @@
+#!/bin/bash
+# SQ / SQC / TCC counter passes (one counter group per rocprofv3 run, as MI355X_MICROARCH.md
+# prescribes) over tools/kbench.py for the kernels matching a regex.
+# usage (GPU box): bash tools/pmc_passes.sh <tag> "<kbench --only regex>"; then
+#   python tools/pmc_table.py gpurun_out/pmc_<tag> <kernel-name-regex>
 set -e
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
