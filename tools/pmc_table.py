@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Mean per-dispatch PMC counters of kernels matching a regex from tools/_pmc.sh pass dirs.
+"""Mean per-dispatch PMC counters of kernels matching a regex from tools/pmc_passes.sh pass dirs.
 usage: python tools/pmc_table.py gpurun_out/pmc_<tag> <kernel-regex>"""
 import collections, csv, glob, re, sys
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
