@@ -223,16 +223,17 @@ class Gate(torch.nn.Module):
         self.cst = cg.silu_normalize2mom()
 
     def forward(self, x):
-        ns, ng = self.irreps_scalars.dim, self.irreps_gates.dim
+        # one torch.split instead of per-block slices: its backward is a single cat, where
+        # slice backwards would each zero-fill a full [n, dim_in] gradient and add it up
+        # (six zero-fill + add pairs per gate; the values are identical either way)
+        gated = [mul * ir.dim for mul, ir in self.irreps_gated]
+        pieces = torch.split(x, [self.irreps_scalars.dim, self.irreps_gates.dim] + gated, dim=1)
         act = torch.nn.functional.silu
-        scalars = self.cst * act(x[:, :ns])
-        gates = self.cst * act(x[:, ns: ns + ng])
-        out, g_off, x_off = [scalars], 0, ns + ng
-        for mul, ir in self.irreps_gated:
-            blk = x[:, x_off: x_off + mul * ir.dim].view(-1, mul, ir.dim)
-            out.append((blk * gates[:, g_off: g_off + mul, None]).reshape(-1, mul * ir.dim))
-            g_off += mul
-            x_off += mul * ir.dim
+        scalars = self.cst * act(pieces[0])
+        gates = torch.split(self.cst * act(pieces[1]), [mul for mul, _ in self.irreps_gated], dim=1)
+        out = [scalars]
+        for (mul, ir), blk, g in zip(self.irreps_gated, pieces[2:], gates):
+            out.append((blk.reshape(-1, mul, ir.dim) * g[:, :, None]).reshape(-1, mul * ir.dim))
         return torch.cat(out, dim=1)
 
 
