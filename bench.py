@@ -227,8 +227,8 @@ def main_cgc(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="graphs per GPU per step")
     ap.add_argument("--nodes", type=int, default=1024)
     ap.add_argument("--edges", type=int, default=4096)
