@@ -9,8 +9,9 @@ all-reduce (N>1, RCCL) + grad-norm clip 10 + AdamW(amsgrad) step.  Graphs are
 sharded by graph id across ranks (weak scaling); inputs are resident in HBM
 before the timed region.
 
-Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 the driver
-uses ``torch.distributed.run`` and each rank reads RANK/LOCAL_RANK/WORLD_SIZE.
+Run: ``python bench.py [--gpus N --steps K --warmup W]``.  For N > 1 the driver uses
+``torch.distributed.run`` and each rank reads RANK/LOCAL_RANK/WORLD_SIZE; without a
+launcher ``--gpus N`` starts the N rank processes itself (``launch_ranks``).
 Rank 0 prints one JSON line (roofline of the fused interaction kernel measured
 with HIP events over the timed region; CPU baseline = the oracle restatement).
 """
@@ -31,6 +32,48 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _spawned_rank(local_rank: int, world: int, port: int, argv):
+    """Entry point of a rank started by ``launch_ranks`` (a fresh interpreter: spawn)."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
+def launch_ranks(n: int) -> None:
+    """``bench.py --gpus N`` without a launcher: start N rank processes (spawn, i.e. fresh
+    interpreters, before this process touches the GPU) and wait for them; they read
+    RANK/LOCAL_RANK/WORLD_SIZE like ranks under ``torch.distributed.run``."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned_rank, args=(n, _free_port(), sys.argv[1:]), nprocs=n, join=True,
+                       start_method="spawn")
+
+
+def init_dist():
+    """(world, rank, local_rank, device, n_devices) of this rank.  One process per GPU over
+    RCCL (backend 'nccl'); when there are fewer visible devices than ranks (a rehearsal on a
+    1-GPU box) the ranks share devices and talk over gloo instead."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if ndev >= world:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local_rank, dev, min(world, ndev)
 
 
 def make_params(layers: int, max_edge_radius: float, lmax: int = 4, storage: str = "float32"):
@@ -72,33 +115,79 @@ def pmc_traffic(kernel: str, args) -> dict | None:
             "source": f"profiles/pmc_traffic.json ({tab['source']})"}
 
 
-def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax: int = 4):
+def host_cpu() -> dict:
+    """The host cores this process may use: the cgroup CPU quota when one is set (the GPU box
+    gives each job a share of a larger machine), else the affinity mask; plus the CPU model."""
+    n_aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": min(n_aff, quota) if quota else n_aff, "os_cpu_count": os.cpu_count(),
+            "affinity": n_aff, "cgroup_quota": quota, "model": model,
+            "isa": torch.backends.cpu.get_cpu_capability()}
+
+
+def _time_cpu_steps(step, budget_s: float, warmup: int, min_steps: int, max_steps: int):
+    """``warmup`` untimed steps, then timed steps until ``min_steps`` are done and the budget is
+    spent, or ``max_steps`` are done (3 warm-up + >= 10 timed)."""
+    for _ in range(warmup):
+        step()
+    times, t_start = [], time.perf_counter()
+    while len(times) < max_steps:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+        if len(times) >= min_steps and time.perf_counter() - t_start > budget_s:
+            break
+    times.sort()
+    return times
+
+
+def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax: int = 4,
+                 full: bool = False):
     """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
     scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
-    shape: fwd + loss + bwd, median over steps within ``budget_s``."""
+    shape: fwd + loss + bwd on all the host cores this job has.  ``full``: BASELINE.md
+    section 2's protocol (3 warm-up + 10 timed steps, ~4 min); default: 1 warm-up and
+    timed steps within ``budget_s`` (at least 1), so that the default bench run stays short."""
     import oracle.model as om
     from oracle.train import stiffness_loss
     from gnn.data import collate
     from gnn.synthetic import SyntheticLattices
+    host = host_cpu()
+    torch.set_num_threads(host["threads"])
     ds = SyntheticLattices(1, n_nodes, n_edges, 1234)
     b = collate([ds[0]])
     torch.manual_seed(0)
     m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius, lmax))
-    times = []
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
+
+    def step():
         m.zero_grad(set_to_none=True)
-        loss = stiffness_loss(m(b)["stiffness"], b.stiffness)
-        loss.backward()
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s or len(times) >= 10:
-            break
-    med = statistics.median(times)
-    return {"value": round(1.0 / med, 4), "unit": "lattice-graphs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+        stiffness_loss(m(b)["stiffness"], b.stiffness).backward()
+
+    warm, lo, hi = (3, 10, 10) if full else (1, 1, 10)
+    t = _time_cpu_steps(step, budget_s, warm, lo, hi)
+    med = statistics.median(t)
+    pct = lambda q: t[min(len(t) - 1, int(q * (len(t) - 1) + 0.5))]  # noqa: E731
+    return {"value": round(1.0 / med, 4), "unit": "lattice-graphs/s", "cores": host["threads"],
+            "kind": "port", "cpu": host,
             "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} edges, "
-                      f"{layers} layers lmax {lmax}, median of {len(times)} step(s) ({med:.2f} s/step)"}
+                      f"{layers} layers lmax {lmax}; {warm} warm-up + {len(t)} timed step(s): median "
+                      f"{med:.2f} s, p10 {pct(0.1):.2f} s, p90 {pct(0.9):.2f} s" +
+                      ("" if full else f" (budget {budget_s:.0f} s; BASELINE.md section 2's 3 + 10 "
+                                        "steps: bench.py --cpu-full)")}
 
 
 def cgc_fwd_bytes(n: int, e: int, d: int) -> int:
@@ -120,31 +209,26 @@ def cpu_baseline_cgc(modified: bool, p, n_nodes: int, n_edges: int, budget_s: fl
     m = (ocgc.CrystGraphConv if modified else ocgc.CrystGraphConvVanilla)(p)
     iu = torch.triu_indices(6, 6)
     tgt = b.stiffness if modified else b.stiffness[:, iu[0], iu[1]]
-    times, t_start = [], time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
+    host = host_cpu()
+    torch.set_num_threads(host["threads"])
+
+    def step():
         m.zero_grad(set_to_none=True)
         stiffness_loss(m(b)["stiffness"], tgt).backward()
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s or len(times) >= 50:
-            break
+
+    times = _time_cpu_steps(step, budget_s, 3, 10, 50)
     med = statistics.median(times)
-    return {"value": round(1.0 / med, 3), "unit": "lattice-graphs/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} "
-                                      f"edges, median of {len(times)} step(s) ({med * 1e3:.1f} ms/step)"}
+    return {"value": round(1.0 / med, 3), "unit": "lattice-graphs/s", "cores": host["threads"],
+            "kind": "port", "cpu": host,
+            "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} "
+                      f"edges, 3 warm-up + median of {len(times)} step(s) ({med * 1e3:.1f} ms/step)"}
 
 
 def main_cgc(args):
     """BASELINE config 4: CGC / mCGC (scripts/train_cgcnn_*.py) on the same synthetic lattices.
     One step = forward + loss + backward + flat all-reduce + AdamW (hidden 128 / 64, 3 passes)."""
     from argparse import Namespace
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    world, rank, local_rank, dev, n_dev = init_dist()
     from gnn import cgc, ops
     from gnn.data import collate
     from gnn.parallel import FlatGradAllReduce, broadcast_parameters
@@ -207,7 +291,7 @@ def main_cgc(args):
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum["cgc_fwd"]["count"]}
         out = {"metric": f"lattice-graphs/s (fwd+bwd), {args.model} 3-layer, ~1k nodes/~4k edges",
                "value": round(world * args.batch * args.steps / dt, 2), "unit": "lattice-graphs/s",
-               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "n_gpus": n_dev, "ranks": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic periodic lattices (SURVEY 8d generator), random-init weights",
@@ -236,6 +320,8 @@ def main():
     ap.add_argument("--lmax", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="CPU baseline with BASELINE.md section 2's 3 warm-up + 10 timed steps")
     ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
     ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"],
                     help="egnn = the headline EnergyEquivGNN; cgc_* = BASELINE config 4 benchmark models")
@@ -247,18 +333,17 @@ def main():
                     help="2 = BASELINE configs[1] (default); 5 = configs[4]: lmax 3, ~5k-node "
                          "lattices (5000 nodes / 20000 edges), bf16 storage, fp32 accumulate")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; "
+              "using WORLD_SIZE", file=sys.stderr)
     if args.config == 5:
         args.lmax, args.nodes, args.edges, args.storage = 3, 5000, 20000, "bfloat16"
     if args.model != "egnn":
         return main_cgc(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    world, rank, local_rank, dev, n_dev = init_dist()
 
     from gnn import EnergyEquivGNN, ops
     from gnn.data import collate
@@ -337,14 +422,16 @@ def main():
                 roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax)
+            cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax,
+                               full=args.cpu_full)
         value = world * args.batch * args.steps / dt
         out = {
             "metric": ("lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU"
                        if args.config == 2 else
                        "lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN lmax 3, ~5k nodes/~20k edges, "
                        "bf16 storage + fp32 accumulate (BASELINE configs[4])"),
-            "value": round(value, 2), "unit": "lattice-graphs/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 2), "unit": "lattice-graphs/s", "n_gpus": n_dev, "ranks": world,
+            "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32" if args.storage == "float32" else "f32 (bf16 storage of w / grad_w / gxe)",

@@ -111,8 +111,15 @@ def ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
-def stream() -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+def stream(t: torch.Tensor) -> ctypes.c_void_p:
+    """The current stream of ``t``'s device.  Kernels launch on the current HIP device, so
+    ``t`` must live there (``torch.cuda.device(...)`` / ``torch.cuda.set_device``)."""
+    dev = t.device
+    cur = torch.cuda.current_device()
+    if dev.index is not None and dev.index != cur:
+        raise EELGError(f"operand on {dev} but the current HIP device is cuda:{cur}; run the "
+                        f"model under torch.cuda.device({dev.index}) or set_device({dev.index})")
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
 def tp_config(name: str) -> Tuple[int, Dict[str, int], int]:

@@ -1,8 +1,11 @@
 """Hot-path blocks of the reference ``gnn/blocks.py``, MI355X-native.
 
-Constructors, module names, parameter names and ``forward`` signatures follow
-the reference, so ``state_dict``s round-trip (the reference's large
-``U_matrix_*`` buffers are derived data and are not stored here).
+Constructors, module names, parameter names, persistent buffers and ``forward``
+signatures follow the reference, so ``state_dict``s round-trip strictly both ways:
+the reference's large ``U_matrix_*`` buffers are derived data, emitted by
+``state_dict()`` and verified / adopted on load (``mace.SymmetricContraction``)
+rather than held on the device; ``Q_flat`` is a real buffer, so a loaded change
+of basis is used as is.
 
 ``edge_index`` arguments accept either the reference's ``[2, E]`` tensor (the
 edge tensors are then in the caller's order and get permuted once) or an
@@ -94,6 +97,24 @@ class Cart_4_to_Mandel(torch.nn.Module):  # noqa: N801
             m[src, r * 6 + q] = mask[r, q]
             m[src, q * 6 + r] = mask[q, r]
         self.register_buffer("map", torch.tensor(m, dtype=torch.float32), persistent=False)
+        # the reference's persistent buffers (same names, shapes and values), so checkpoints
+        # round-trip strictly; they are verified on load, the GEMM above is what runs
+        self.register_buffer("mask", torch.tensor(mask, dtype=torch.get_default_dtype()))
+        rows_t, cols_t = torch.triu_indices(6, 6)
+        self.register_buffer("rows", rows_t)
+        self.register_buffer("cols", cols_t)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        for name in ("mask", "rows", "cols"):
+            t = state_dict.get(prefix + name)
+            mine = getattr(self, name)
+            if t is not None and (t.shape != mine.shape or not torch.allclose(
+                    t.detach().cpu().double(), mine.cpu().double(), rtol=1e-6, atol=0)):
+                error_msgs.append(f"{prefix}{name}: differs from the reference's Cart_4_to_Mandel "
+                                  "tables (gnn/blocks.py:395-417); refusing to load")
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
 
     def forward(self, c):
         return (c.reshape(c.shape[0], 81) @ self.map).view(c.shape[0], 6, 6)

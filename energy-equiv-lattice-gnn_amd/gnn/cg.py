@@ -300,6 +300,68 @@ def symcon_plan(coupling: str, out_ls: Tuple[int, ...], correlation: int) -> Sym
     return SymConPlan(Dout, tuple(out_ls), tuple(keys), ubig, tuple(blocks))
 
 
+def reference_U_shape(coupling: str, l_out: int, nu: int) -> Tuple[int, ...]:
+    """Shape of the reference's ``U_matrix_{nu}`` buffer (``gnn/mace.py:198-205``): the
+    stacked [2l+1, D x nu, K] tensor with ``squeeze()`` applied per path before stacking
+    (``:462-476``), so the leading 1 of l_out = 0 is dropped."""
+    u = U_matrix(coupling, l_out, nu)
+    return tuple(u.shape[1:]) if u.shape[0] == 1 else tuple(u.shape)
+
+
+def symcon_block_from_U(plan: SymConPlan, l_out: int, nu: int, u: np.ndarray,
+                        tol: float = 1e-6) -> Tuple[int, np.ndarray]:
+    """(first column, [nterms, K] values) of the (l_out, nu) weight block of ``plan.ubig``,
+    recomputed from a U tensor given in ANY basis of that block ([2l+1, D x nu, K], or the
+    reference's squeezed shape).
+
+    The symmetric contraction only sees U through its symmetrisation over the nu input
+    slots, summed per monomial class: ``row(cls, m) = sum over distinct permutations p of
+    cls of U[m, p]`` (``symcon_plan``).  Raises ValueError when the symmetrised U has weight
+    on a (class, component) the generated kernels have no term for: such a basis is not
+    representable, and silently dropping it would change the model."""
+    m_dim = 2 * l_out + 1
+    u = np.asarray(u, dtype=np.float64)
+    if u.ndim == nu + 1:                       # squeezed l_out = 0 form
+        u = u[None]
+    if u.shape[0] != m_dim or u.ndim != nu + 2:
+        raise ValueError(f"U for l={l_out}, nu={nu}: unexpected shape {u.shape}")
+    D = u.shape[1]
+    k = u.shape[-1]
+    kt0 = 0
+    for l, n, kk in plan.weight_blocks:
+        if (l, n) == (l_out, nu):
+            if kk != k:
+                raise ValueError(f"U for l={l_out}, nu={nu}: {k} basis columns, expected {kk}")
+            break
+        kt0 += kk
+    else:
+        raise ValueError(f"no weight block (l={l_out}, nu={nu}) in the plan")
+    sym = np.zeros_like(u)
+    for p in itertools.permutations(range(1, nu + 1)):
+        sym += np.transpose(u, (0,) + p + (nu + 1,))
+    fact = math.factorial(nu)
+    off = 0
+    for l in plan.ls:
+        if l == l_out:
+            break
+        off += 2 * l + 1
+    want = {(cls[:nu], o - off): i for i, (n, cls, o) in enumerate(plan.terms)
+            if n == nu and off <= o < off + m_dim}
+    block = np.zeros((len(plan.terms), k))
+    scale = max(np.abs(u).max(), 1e-300)
+    for cls in _sym_classes(D, nu):
+        n_distinct = len(set(itertools.permutations(cls)))
+        acc = sym[(slice(None),) + cls] * (n_distinct / fact)      # [2l+1, K]
+        for m in range(m_dim):
+            i = want.get((tuple(cls), m))
+            if i is not None:
+                block[i] = acc[m]
+            elif np.abs(acc[m]).max() > tol * scale:
+                raise ValueError(f"U for l={l_out}, nu={nu} has a symmetric component on monomial "
+                                 f"{cls} -> m={m}, which the generated kernels do not evaluate")
+    return kt0, block
+
+
 # --------------------------------------------------------------------------
 # Rank-4 stiffness change of basis ('2x0e+2x2e+1x4e' -> 3x3x3x3)
 # --------------------------------------------------------------------------

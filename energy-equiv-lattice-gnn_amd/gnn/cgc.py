@@ -46,7 +46,7 @@ class _CGCConv(torch.autograd.Function):
         tok = ops.TIMER.start("cgc_fwd")
         _lib.check(_lib.load().eelg_cgc_fwd(
             _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ep), _lib.ptr(csr.sender), _lib.ptr(csr.rowptr),
-            _lib.ptr(row_scale), n, d, _lib.ptr(agg), _lib.stream()), "cgc_fwd")
+            _lib.ptr(row_scale), n, d, _lib.ptr(agg), _lib.stream(agg)), "cgc_fwd")
         ops.TIMER.stop(tok)
         ctx.save_for_backward(x, edge_ft, ps, pr, ep, w, row_scale)
         ctx.csr = csr
@@ -63,7 +63,7 @@ class _CGCConv(torch.autograd.Function):
         tok = ops.TIMER.start("cgc_bwd")
         _lib.check(_lib.load().eelg_cgc_bwd(
             _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ep), _lib.ptr(csr.sender), _lib.ptr(csr.rowptr),
-            _lib.ptr(row_scale), n, d, _lib.ptr(g), _lib.ptr(dz), _lib.ptr(gr), _lib.stream()), "cgc_bwd")
+            _lib.ptr(row_scale), n, d, _lib.ptr(g), _lib.ptr(dz), _lib.ptr(gr), _lib.stream(g)), "cgc_bwd")
         ops.TIMER.stop(tok)
         gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)   # per-sender sums of dz
         ws, wr, we = w[:, :d], w[:, d: 2 * d], w[:, 2 * d:]

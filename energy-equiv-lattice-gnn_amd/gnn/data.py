@@ -52,6 +52,8 @@ class Data:
     def to(self, device, non_blocking: bool = False) -> "Data":
         out = self.__class__()
         for k, v in self.__dict__.items():
+            if k.startswith("_eelg"):          # per-object caches (the model's CSR) stay behind
+                continue
             setattr(out, k, v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v)
         return out
 
@@ -106,13 +108,12 @@ def build_edge_csr(edge_index: torch.Tensor, num_nodes: int) -> Dict[str, torch.
     perm = torch.sort(rcv, stable=True).indices
     s_sorted = snd[perm]
     r_sorted = rcv[perm]
-    cnt = torch.bincount(r_sorted, minlength=num_nodes)
-    rowptr = torch.zeros(num_nodes + 1, dtype=torch.int64, device=dev)
-    rowptr[1:] = torch.cumsum(cnt, 0)
-    sperm = torch.sort(s_sorted, stable=True).indices
-    scnt = torch.bincount(s_sorted, minlength=num_nodes)
-    srowptr = torch.zeros(num_nodes + 1, dtype=torch.int64, device=dev)
-    srowptr[1:] = torch.cumsum(scnt, 0)
+    # segment bounds of sorted keys by searchsorted: unlike bincount (which sizes its output
+    # from the data) this never waits for the device
+    bounds = torch.arange(num_nodes + 1, device=dev, dtype=r_sorted.dtype)
+    rowptr = torch.searchsorted(r_sorted, bounds)
+    sorted_s, sperm = torch.sort(s_sorted, stable=True)
+    srowptr = torch.searchsorted(sorted_s, bounds)
     return {
         "perm": perm,
         "rowptr": rowptr.to(torch.int32),
@@ -120,7 +121,6 @@ def build_edge_csr(edge_index: torch.Tensor, num_nodes: int) -> Dict[str, torch.
         "receiver": r_sorted.to(torch.int32).contiguous(),
         "sperm": sperm.to(torch.int32).contiguous(),
         "srowptr": srowptr.to(torch.int32),
-        "max_in_degree": int(cnt.max().item()) if cnt.numel() else 0,
     }
 
 

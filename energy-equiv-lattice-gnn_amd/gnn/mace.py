@@ -68,6 +68,60 @@ class SymmetricContraction(torch.nn.Module):
             self.contractions[f"{mul}x{ir}"] = Contraction(ks[ir.l], self.mul)
         self.register_buffer("u_sym", torch.tensor(plan.ubig, dtype=torch.float32), persistent=False)
         self._cfg = None
+        self._coupling, self._ls = coupling, ls
+        self._u_loaded = {}          # (l, nu) -> U adopted from a loaded state_dict (CPU f32)
+        self._register_state_dict_hook(SymmetricContraction._emit_reference_U)
+
+    # -- reference checkpoints (gnn/mace.py:198-205: U_matrix_{nu} buffers per Contraction) --
+    def _u_keys(self, prefix: str):
+        for mul, ir in self.irreps_out:
+            for nu in range(1, self.correlation + 1):
+                yield ir.l, nu, f"{prefix}contractions.{mul}x{ir}.U_matrix_{nu}"
+
+    @staticmethod
+    def _emit_reference_U(module, state_dict, prefix, local_metadata):
+        """``state_dict()`` carries the reference's U buffers too (derived data, not held on
+        the device), so a checkpoint of this model loads strictly into the reference."""
+        for l, nu, key in module._u_keys(prefix):
+            u = module._u_loaded.get((l, nu))
+            if u is None:
+                shape = cg.reference_U_shape(module._coupling, l, nu)
+                u = torch.tensor(cg.U_matrix(module._coupling, l, nu), dtype=torch.float32).reshape(shape)
+            state_dict[key] = u
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        """Accepts the reference's ``U_matrix_{nu}`` buffers.  A U equal to the derived one
+        (to fp32 accuracy) is simply verified.  A U in another basis of the same space (e.g.
+        a different path order or sign convention) is adopted: its symmetrisation replaces
+        the matching block of ``u_sym``, so the contraction computes exactly what the
+        reference computes with that U and the loaded weights.  A U with symmetric weight on
+        monomials the generated kernels do not evaluate raises."""
+        for l, nu, key in list(self._u_keys(prefix)):
+            if key not in state_dict:
+                continue
+            u = state_dict.pop(key).detach().to("cpu", torch.float64)
+            want = cg.reference_U_shape(self._coupling, l, nu)
+            if tuple(u.shape) != want:
+                error_msgs.append(f"size mismatch for {key}: copying a param with shape "
+                                  f"{tuple(u.shape)}, the reference shape is {want}")
+                continue
+            ref = torch.from_numpy(cg.U_matrix(self._coupling, l, nu)).reshape(want)
+            if float((u - ref).abs().max()) <= 1e-6 * float(ref.abs().max()):
+                self._u_loaded.pop((l, nu), None)
+                continue
+            plan = cg.symcon_plan(self._coupling, self._ls, self.correlation)
+            try:
+                k0, block = cg.symcon_block_from_U(plan, l, nu, u.numpy())
+            except ValueError as e:
+                error_msgs.append(f"{key}: {e}")
+                continue
+            with torch.no_grad():
+                self.u_sym[:, k0: k0 + block.shape[1]] = torch.from_numpy(block).to(self.u_sym)
+            self._u_csr = None
+            self._u_loaded[(l, nu)] = u.to(torch.float32)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
 
     def _config(self):
         if self._cfg is None:

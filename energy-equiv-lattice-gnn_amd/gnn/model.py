@@ -86,6 +86,10 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         main = torch.cuda.current_stream(edge_feats.device)
         side = ops.side_stream(edge_feats.device)
         side.wait_stream(main)
+        # edge_feats is made on the main stream and read (and saved for the MLP backward) on
+        # the side stream: without this the allocator could hand its block to a main-stream
+        # allocation while a side-stream kernel still reads it
+        edge_feats.record_stream(side)
         ws, evs = [], []
         with torch.cuda.stream(side):
             for layer in self.layers:
@@ -134,9 +138,13 @@ class EnergyEquivGNN(torch.nn.Module):
     def edge_graph(batch) -> ops.EdgeCSR:
         """Receiver-sorted CSR of ``batch.edge_index`` on its device (cached on the batch)."""
         n = batch.node_attrs.shape[0]
-        dev = batch.edge_index.device
+        ei = batch.edge_index
+        dev = ei.device
+        # the cache is valid only for this very edge_index: same storage, no in-place edits
+        # since (autograd version counter), same node and edge counts, same device
+        key = (ei.data_ptr(), ei._version, tuple(ei.shape), n, str(dev))
         cached = getattr(batch, "_eelg_csr", None)
-        if cached is not None and cached.sender.device == dev and cached.num_nodes == n:
+        if cached is not None and getattr(batch, "_eelg_csr_key", None) == key:
             return cached
         pre = getattr(batch, "csr", None)
         if isinstance(pre, dict) and torch.is_tensor(pre.get("perm")):
@@ -146,11 +154,20 @@ class EnergyEquivGNN(torch.nn.Module):
             csr = ops.EdgeCSR.build(batch.edge_index, n)
         try:
             batch._eelg_csr = csr
+            batch._eelg_csr_key = key
         except AttributeError:
             pass
         return csr
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
+        dev = batch.positions.device
+        if dev.type != "cuda":
+            raise RuntimeError("the EnergyEquivGNN hot path runs only on a HIP device "
+                               "(got a CPU batch); move the model and batch to 'cuda'")
+        with torch.cuda.device(dev):        # kernels launch on the batch's device
+            return self._forward(batch)
+
+    def _forward(self, batch) -> Dict[str, torch.Tensor]:
         csr = self.edge_graph(batch)
         node_ft = self.node_ft_embedding(batch.node_attrs)
         shifts = batch.shifts[csr.perm]

@@ -21,6 +21,19 @@ from . import cg
 from .irreps import Irreps
 
 
+def _accept_output_mask(state_dict, key: str, irreps_out, covered, error_msgs) -> None:
+    """e3nn's ``Linear`` / ``TensorProduct`` register an ``output_mask`` buffer (1 on the output
+    irreps some instruction writes).  Reference checkpoints may carry it: it is derived data,
+    so it is accepted and checked against this module's instructions, not stored."""
+    m = state_dict.pop(key, None)
+    if m is None:
+        return
+    want = torch.cat([torch.full((mul * ir.dim,), 1.0 if o in covered else 0.0)
+                      for o, (mul, ir) in enumerate(irreps_out)]) if irreps_out.dim else torch.ones(0)
+    if tuple(m.shape) != tuple(want.shape) or not torch.equal(m.detach().cpu().float() != 0, want != 0):
+        error_msgs.append(f"{key}: output mask does not match the module's instructions")
+
+
 class _OnStream(torch.autograd.Function):
     """Identity (a view) applied while ``stream`` is current, so that autograd runs its
     backward -- and the gradient accumulation of the parameter behind it -- on ``stream``."""
@@ -91,6 +104,13 @@ class Linear(torch.nn.Module):
         self._in_off, self._out_off = self.irreps_in.offsets(), self.irreps_out.offsets()
         self._build_descriptors()
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        _accept_output_mask(state_dict, prefix + "output_mask", self.irreps_out,
+                            {o for _, o in self.instructions}, error_msgs)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
     # -- descriptor tables for the C ABI (built once) ---------------------------
     def _build_descriptors(self):
         from . import _lib
@@ -159,7 +179,7 @@ class Linear(torch.nn.Module):
         self._fwd_desc.max_rows = n * self._fwd_maxd
         _lib.check(_lib.load().eelg_linear_fwd(
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(weight), _lib.ptr(bias), n, _lib.ptr(y),
-            self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream()), "linear_fwd")
+            self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream(y)), "linear_fwd")
         return y
 
     def _bwd_x(self, gy, weight):
@@ -169,7 +189,7 @@ class Linear(torch.nn.Module):
         self._bx_desc.max_rows = n * self._bx_maxd
         _lib.check(_lib.load().eelg_linear_fwd(
             _lib.ptr(gy), self.irreps_out.dim, _lib.ptr(weight), None, n, _lib.ptr(gx),
-            self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream()), "linear_bwd_x")
+            self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream(gx)), "linear_bwd_x")
         return gx
 
     def _bwd_w(self, x, gy):
@@ -185,7 +205,7 @@ class Linear(torch.nn.Module):
         part = torch.empty(slices, self.weight_numel, device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().eelg_linear_bwd_w(
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, nps,
-            _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream()),
+            _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream(part)),
             "linear_bwd_w")
         return part.sum(0)
 
@@ -222,6 +242,14 @@ class Gate(torch.nn.Module):
         self.irreps_out = self.irreps_scalars + self.irreps_gated
         self.cst = cg.silu_normalize2mom()
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        # e3nn's Gate multiplies with an ElementwiseTensorProduct submodule ``mul``
+        _accept_output_mask(state_dict, prefix + "mul.output_mask", self.irreps_gated,
+                            set(range(len(self.irreps_gated))), error_msgs)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
     def forward(self, x):
         # one torch.split instead of per-block slices: its backward is a single cat, where
         # slice backwards would each zero-fill a full [n, dim_in] gradient and add it up
@@ -247,3 +275,10 @@ class TensorProduct(torch.nn.Module):
         self.instructions = list(instructions)
         self.weight_numel = sum(self.irreps_in1[i1].mul * self.irreps_in2[i2].mul
                                 for i1, i2, *_ in self.instructions)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        _accept_output_mask(state_dict, prefix + "output_mask", self.irreps_out,
+                            {ins[2] for ins in self.instructions}, error_msgs)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)

@@ -131,7 +131,7 @@ def edge_embed(pos, csr: EdgeCSR, shifts_sorted, radius_sorted, lmax: int, nb: i
     _lib.check(lib.eelg_edge_embed(
         _lib.ptr(_f32(pos)), _lib.ptr(csr.sender), _lib.ptr(csr.receiver),
         _lib.ptr(_f32(shifts_sorted)), _lib.ptr(_f32(radius_sorted)), e, lmax, nb,
-        float(len_end), float(rad_end), _lib.ptr(sh), _lib.ptr(feats), _lib.stream()), "edge_embed")
+        float(len_end), float(rad_end), _lib.ptr(sh), _lib.ptr(feats), _lib.stream(sh)), "edge_embed")
     return sh[:, :nsh], feats          # [E, nsh] view of the padded rows the TP kernels read
 
 
@@ -166,7 +166,7 @@ def segment_sum_csr(src, rowptr, n_rows: int, idx=None, row_scale=None, scale: f
     lib = _lib.load()
     fn = lib.eelg_segment_sum_csr_bf16 if bf else lib.eelg_segment_sum_csr
     _lib.check(fn(_lib.ptr(src), _lib.ptr(rowptr), _lib.ptr(idx), _lib.ptr(row_scale), float(scale),
-                  n_rows, int(width), _lib.ptr(out), _lib.stream()), "segment_sum_csr")
+                  n_rows, int(width), _lib.ptr(out), _lib.stream(out)), "segment_sum_csr")
     return out
 
 
@@ -183,7 +183,7 @@ def segment_sum_long(src: torch.Tensor, rowptr: torch.Tensor, n_rows: int,
     tok = TIMER.start("segment_sum_split")
     _lib.check(_lib.load().eelg_segment_sum_split(
         _lib.ptr(src), _lib.ptr(rowptr), None, _lib.ptr(row_scale), float(scale), n_rows, width,
-        n_split, _lib.ptr(work), _lib.ptr(out), _lib.stream()), "segment_sum_split")
+        n_split, _lib.ptr(work), _lib.ptr(out), _lib.stream(out)), "segment_sum_split")
     TIMER.stop(tok)
     return out
 
@@ -244,7 +244,7 @@ class _TPInteraction(torch.autograd.Function):
         tok = TIMER.start(f"tp_fwd[din={info['din']}]")
         fwd = lib.eelg_tp_fwd_bf16 if bf else lib.eelg_tp_fwd
         _lib.check(fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
-                       _lib.ptr(csr.rowptr), n, float(inv_norm), _lib.ptr(agg), _lib.stream()),
+                       _lib.ptr(csr.rowptr), n, float(inv_norm), _lib.ptr(agg), _lib.stream(agg)),
                    "tp_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, sh, w)
@@ -264,7 +264,7 @@ class _TPInteraction(torch.autograd.Function):
         tok = TIMER.start(f"tp_bwd[din={info['din']}]")
         _lib.check(bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
                        _lib.ptr(csr.receiver), e, _lib.ptr(g), float(ctx.inv_norm), _lib.ptr(gw),
-                       _lib.ptr(gxe), _lib.stream()), "tp_bwd")
+                       _lib.ptr(gxe), _lib.stream(gxe)), "tp_bwd")
         TIMER.stop(tok)
         gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
         return gx, None, gw, None, None, None, None
@@ -289,7 +289,7 @@ class _SymCon(torch.autograd.Function):
         lib = _lib.load()
         tok = TIMER.start("sc_fwd")
         _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),
-                                   _lib.stream()), "sc_fwd")
+                                   _lib.stream(out)), "sc_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, coef)
         ctx.cfg, ctx.info, ctx.mul, ctx.side = cfg, info, mul, side
@@ -317,9 +317,9 @@ class _SymCon(torch.autograd.Function):
                 t.record_stream(side)
             with torch.cuda.stream(side):
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
-                                              _lib.stream()), "sc_cmajor")
+                                              _lib.stream(xt)), "sc_cmajor")
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
-                                              _lib.stream()), "sc_cmajor")
+                                              _lib.stream(gt)), "sc_cmajor")
         if want_x:
             gx = torch.empty_like(x)
             tok = TIMER.start("sc_bwd_x")
@@ -327,16 +327,16 @@ class _SymCon(torch.autograd.Function):
             _lib.check(lib.eelg_sc_bwd_x_cm(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
                                             ctx.mul, _lib.ptr(gx),
                                             _lib.ptr(xt) if fuse else None,
-                                            _lib.ptr(gt) if fuse else None, _lib.stream()),
+                                            _lib.ptr(gt) if fuse else None, _lib.stream(gx)),
                        "sc_bwd_x")
             TIMER.stop(tok)
         if want_c:
             if not (want_x or cm_side):
                 tok = TIMER.start("sc_cmajor")
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
-                                              _lib.stream()), "sc_cmajor")
+                                              _lib.stream(xt)), "sc_cmajor")
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
-                                              _lib.stream()), "sc_cmajor")
+                                              _lib.stream(gt)), "sc_cmajor")
                 TIMER.stop(tok)
             chunk = max(256, min(4096, (n // 16 + 255) // 256 * 256))   # a multiple of the tile
             nch = (n + chunk - 1) // chunk
@@ -352,7 +352,7 @@ class _SymCon(torch.autograd.Function):
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 tok = TIMER.start("sc_bwd_coef")
                 _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul,
-                                                chunk, _lib.ptr(part), _lib.stream()), "sc_bwd_coef")
+                                                chunk, _lib.ptr(part), _lib.stream(part)), "sc_bwd_coef")
                 TIMER.stop(tok)
                 gcoef = part.sum(0)
         return gx, gcoef, None, None, None, None
@@ -494,7 +494,7 @@ def _spmm(trip, n_rows, B, ldb_r, ldb_c, n_cols, out, ldo_r, ldo_c):
     rp, col, val = trip
     _lib.check(_lib.load().eelg_csr_spmm(_lib.ptr(rp), _lib.ptr(col), _lib.ptr(val), n_rows,
                                          _lib.ptr(B), ldb_r, ldb_c, n_cols, _lib.ptr(out), ldo_r,
-                                         ldo_c, _lib.stream()), "csr_spmm")
+                                         ldo_c, _lib.stream(out)), "csr_spmm")
 
 
 class _SymConCoef(torch.autograd.Function):

@@ -165,5 +165,20 @@ class SymmetricContraction(torch.nn.Module):
         for mul, ir in self.irreps_out:  # keys as the reference: str(irrep_out) == '32x0e'
             self.contractions[f"{mul}x{ir}"] = Contraction(self.irreps_in, Irreps(str(ir)), correlation)
 
-    def forward(self, x):
+    # Test-only memory bound (tests/test_gpu_fullsize.py): > 0 evaluates node chunks of this
+    # size under activation checkpointing.  Every node's arithmetic is unchanged (the
+    # contraction is node-wise); only the [nodes, 32, 2l+1, 25, 25] intermediates are
+    # recomputed in the backward instead of held (~48 GB for one 1k-node 4-layer graph in
+    # fp64).  0 (default) keeps the reference's cost structure for the CPU baseline.
+    node_chunk = 0
+
+    def _forward(self, x):
         return torch.cat([self.contractions[f"{m}x{ir}"](x) for m, ir in self.irreps_out], dim=-1)
+
+    def forward(self, x):
+        c = SymmetricContraction.node_chunk
+        if c and x.shape[0] > c:
+            from torch.utils.checkpoint import checkpoint
+            return torch.cat([checkpoint(self._forward, xc, use_reentrant=False)
+                              for xc in x.split(c)], dim=0)
+        return self._forward(x)
