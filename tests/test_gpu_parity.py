@@ -292,7 +292,7 @@ def test_symcon_grad_x_writes_channel_major_copies(n):
     gx0, gx1 = torch.empty_like(x), torch.empty_like(x)
     xt0, gt0 = torch.empty(800, n, device=DEV), torch.empty(800, n, device=DEV)
     xt1, gt1 = torch.full((800, n), 7.0, device=DEV), torch.full((800, n), 7.0, device=DEV)
-    s = _lib.stream()
+    s = _lib.stream(x)
     _lib.check(lib.eelg_sc_bwd_x(idx, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n, 32,
                                  _lib.ptr(gx0), s), "bwd_x")
     _lib.check(lib.eelg_sc_cmajor(idx, 0, _lib.ptr(x), n, 32, _lib.ptr(xt0), s), "cm")

@@ -102,7 +102,7 @@ def main():
         ops._lib.check(lib.eelg_tp_bwd(idx, ops._lib.ptr(x), ops._lib.ptr(sh), ops._lib.ptr(w),
                                        ops._lib.ptr(csr.sender), ops._lib.ptr(csr.receiver), e,
                                        ops._lib.ptr(g), 0.25, ops._lib.ptr(gw), ops._lib.ptr(gxe),
-                                       ops._lib.stream()), "tp_bwd")
+                                       ops._lib.stream(x)), "tp_bwd")
     bwd_bytes = 4 * (n * 800 + e * 25 + 2 * e * info["wn"] + 2 * e + e * 800 + n * info["dmid"])
     rec("tp_bwd (B)", timeit_if("tp_bwd (B)", tpb, args.reps), bwd_bytes, 2 * tp_flops)
     rec("segment_sum gxe->gx (800)", timeit_if("segment_sum gxe->gx (800)", lambda: ops.segment_sum_csr(gxe, csr.srowptr, n, idx=csr.sperm), args.reps),
@@ -123,24 +123,24 @@ def main():
 
     def scbx():
         ops._lib.check(lib.eelg_sc_bwd_x(sidx, ops._lib.ptr(xs), ops._lib.ptr(coef), ops._lib.ptr(gs), n,
-                                         32, ops._lib.ptr(gx), ops._lib.stream()), "bx")
+                                         32, ops._lib.ptr(gx), ops._lib.stream(x)), "bx")
     rec("sc_bwd_x", timeit_if("sc_bwd_x", scbx, args.reps), 4 * 3 * n * 800, 2 * n * 32 * (nt + 2 * 3250))
     xt = torch.empty(800, n, device=dev)
     gt = torch.empty(800, n, device=dev)
 
     def cm():
         ops._lib.check(lib.eelg_sc_cmajor(sidx, 0, ops._lib.ptr(xs), n, 32, ops._lib.ptr(xt),
-                                          ops._lib.stream()), "cm")
+                                          ops._lib.stream(x)), "cm")
     rec("sc_cmajor", timeit_if("sc_cmajor", cm, args.reps), 4 * 2 * n * 800)
     cm()
-    ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream()), "cm")
+    ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream(x)), "cm")
     chunk = max(256, min(4096, (n // 16 + 255) // 256 * 256))    # as gnn/ops.py
     nch = (n + chunk - 1) // chunk
     part = torch.empty(nch, 32, nt, device=dev)
 
     def scbc():
         ops._lib.check(lib.eelg_sc_bwd_coef(sidx, ops._lib.ptr(xt), ops._lib.ptr(gt), n, 32, chunk,
-                                            ops._lib.ptr(part), ops._lib.stream()), "bc")
+                                            ops._lib.ptr(part), ops._lib.stream(x)), "bc")
     rec("sc_bwd_coef", timeit_if("sc_bwd_coef", scbc, args.reps), None, 2 * n * 32 * (nt + 3250))
     for name, ii, oo in [("lin 800->800", hid, hid),
                          ("lin 7360->800", "160x0e+256x1o+320x2e+320x3o+288x4e", hid)]:
