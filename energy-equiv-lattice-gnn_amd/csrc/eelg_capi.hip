@@ -19,7 +19,7 @@
 
 static thread_local char g_err[512] = "";
 
-static int fail(int code, const char* fmt, ...) {
+int eelg_fail(int code, const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
@@ -27,11 +27,14 @@ static int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-static int check_launch(const char* what) {
+int eelg_check_launch(const char* what) {
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(-3, "%s: launch failed: %s", what, hipGetErrorString(e));
+  if (e != hipSuccess) return eelg_fail(-3, "%s: launch failed: %s", what, hipGetErrorString(e));
   return 0;
 }
+
+#define fail eelg_fail
+#define check_launch eelg_check_launch
 
 // ---------------------------------------------------------------------------
 // edge embedding: one thread per edge

@@ -46,6 +46,10 @@ struct eelg_sc_cfg {
 
 const eelg_tp_cfg* eelg_tp_table(int* n);
 
+// error reporting shared by the translation units of libeelg.so (eelg_capi.hip)
+int eelg_fail(int code, const char* fmt, ...);
+int eelg_check_launch(const char* what);
+
 // bf16 <-> fp32: the widening is exact; the narrowing rounds to nearest even
 // (v_cvt_pk_bf16_f32 on gfx950)
 __device__ __forceinline__ float eelg_bf2f(unsigned short v) { return __uint_as_float((unsigned)v << 16); }

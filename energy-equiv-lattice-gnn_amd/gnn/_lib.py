@@ -45,6 +45,9 @@ _SIGS = {
     "eelg_sc_cmajor": ([_I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
+    "eelg_radial_plan": ([_I, _I, _P, _P], _I),
+    "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
+    "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
 }
 
 LIN_MAXSRC, LIN_MAXSLOT, LINW_MAXINS = 4, 8, 8
@@ -72,6 +75,14 @@ class LinWIns(ctypes.Structure):
 class LinWDesc(ctypes.Structure):
     _fields_ = [("n_ins", _I), ("max_jt", _I), ("max_ut", _I), ("max_rows", _I),
                 ("ins", LinWIns * LINW_MAXINS)]
+
+RADIAL_MAXH = 3
+
+
+class RadialDesc(ctypes.Structure):
+    _fields_ = [("n_feat", _I), ("hidden", _I), ("n_hidden", _I), ("n_out", _I),
+                ("w", _P * RADIAL_MAXH), ("b", _P * RADIAL_MAXH)]
+
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

@@ -174,6 +174,12 @@ class TensorProductInteractionBlock(torch.nn.Module):
             self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
         self.conv_tp = TensorProduct(self._node_feats_irreps, self.edge_attrs_irreps, irreps_mid,
                                      instructions)
+        # the fused radial-MLP kernels (csrc/eelg_radial.hip) are built for these shapes
+        n_feat = self.edge_feats_irreps.num_irreps
+        if MLP_dim not in (32, 64) or not 2 <= MLP_layers <= 4 or not 1 <= n_feat <= 32:
+            raise ValueError(f"radial MLP {n_feat}->{MLP_dim}x{MLP_layers - 1}: the HIP kernels are "
+                             "built for inter_MLP_dim 32 or 64, inter_MLP_layers 2..4 and <= 32 "
+                             "edge features")
         layer = torch.nn.Linear(MLP_dim, self.conv_tp.weight_numel, bias=False)
         torch.nn.init.xavier_uniform_(layer.weight, gain=10)
         self.conv_tp_weights = torch.nn.Sequential(

@@ -5,6 +5,7 @@ There is no eager/CPU fallback: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -396,51 +397,72 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
                                                    dtype=acc)
 
 
+def _radial_desc(params, n_feat: int):
+    n_hidden = (len(params) - 1) // 2
+    hidden = params[0].shape[0]
+    n_out = params[-1].shape[0]
+    d = _lib.RadialDesc()
+    d.n_feat, d.hidden, d.n_hidden, d.n_out = n_feat, hidden, n_hidden, n_out
+    for i in range(n_hidden):
+        d.w[i] = params[2 * i].data_ptr()
+        d.b[i] = params[2 * i + 1].data_ptr()
+    return d
+
+
 class _RadialMLP(torch.autograd.Function):
-    """Linear(+bias)-SiLU-...-Linear(no bias) on edge features (no grad w.r.t. the
-    features, which come from eelg_edge_embed without grad).  Saves the
-    pre-activations; weight gradients use the split-K form above."""
+    """Linear(+bias)-SiLU-...-Linear(no bias) on edge features as one fused HIP kernel
+    (``eelg_radial_fwd``: fp32 MFMA, hidden activations in LDS, only the pre-activations
+    and the [E, W] output reach HBM), backward as two (``eelg_radial_bwd``).  No grad w.r.t.
+    the features, which come from eelg_edge_embed without grad."""
 
     @staticmethod
     def forward(ctx, feats, out_dtype, *params):
-        n_hidden = (len(params) - 1) // 2
-        h, zs, hs = feats, [], [feats]
-        for i in range(n_hidden):
-            z = torch.addmm(params[2 * i + 1], h, params[2 * i].t())
-            h = torch.nn.functional.silu(z)
-            zs.append(z)
-            hs.append(h)
-        if out_dtype == torch.bfloat16:
-            # the [E, W] output layer as a bf16 GEMM (fp32 accumulate), bf16 result
-            hs[-1] = h = h.to(torch.bfloat16)
-            out = h @ params[-1].to(torch.bfloat16).t()
-        else:
-            out = h @ params[-1].t()
-        ctx.save_for_backward(*params, *zs, *hs)
-        ctx.n_hidden = n_hidden
+        _require_device(feats)
+        feats = _f32(feats)
+        params = tuple(_f32(p) for p in params)
+        e, nf = feats.shape
+        d = _radial_desc(params, nf)
+        wo = params[-1]
+        if wo.shape[1] != d.hidden or any(p.shape[0] != d.hidden for p in params[:-1]):
+            raise ValueError("radial MLP: hidden widths differ between layers")
+        zsave = torch.empty(d.n_hidden, e, d.hidden, device=feats.device, dtype=torch.float32)
+        out = torch.empty(e, d.n_out, device=feats.device, dtype=out_dtype)
+        wo_t = wo.t().contiguous()
+        lib = _lib.load()
+        _lib.check(lib.eelg_radial_fwd(_lib.ptr(feats), e, ctypes.byref(d), _lib.ptr(wo_t),
+                                       int(out_dtype == torch.bfloat16), _lib.ptr(zsave),
+                                       _lib.ptr(out), _lib.stream(feats)), "radial_fwd")
+        ctx.save_for_backward(feats, zsave, *params)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        n = ctx.n_hidden
-        saved = ctx.saved_tensors
-        params = saved[: 2 * n + 1]
-        zs = saved[2 * n + 1: 3 * n + 1]
-        hs = saved[3 * n + 1:]
+        feats, zsave, *params = ctx.saved_tensors
         g = g.contiguous()
-        grads = [None] * len(params)
-        if g.dtype == torch.bfloat16:
-            grads[-1] = _wgrad(g, hs[-1].to(torch.bfloat16)).float()
-            gh = (g @ params[-1].to(torch.bfloat16)).float()
-        else:
-            grads[-1] = _wgrad(g, hs[-1])                  # [W, hidden]
-            gh = g @ params[-1]
-        for i in range(n - 1, -1, -1):
-            gz = torch.ops.aten.silu_backward(gh, zs[i])
-            grads[2 * i] = _wgrad(gz, hs[i])
-            grads[2 * i + 1] = gz.sum(0)
-            if i > 0:
-                gh = gz @ params[2 * i]
+        e, nf = feats.shape
+        d = _radial_desc(params, nf)
+        lib = _lib.load()
+        npart, ns = ctypes.c_int(), ctypes.c_int()
+        _lib.check(lib.eelg_radial_plan(e, d.n_out, ctypes.byref(npart), ctypes.byref(ns)),
+                   "radial_plan")
+        h = d.hidden
+        n_small = h * nf + h + (d.n_hidden - 1) * (h * h + h)
+        part_h = torch.empty(npart.value, n_small, device=g.device, dtype=torch.float32)
+        part_wo = torch.empty(ns.value, d.n_out, h, device=g.device, dtype=torch.float32)
+        grad_h = torch.empty(e, h, device=g.device, dtype=torch.float32)
+        if e == 0:
+            part_h.zero_()
+            part_wo.zero_()
+        _lib.check(lib.eelg_radial_bwd(_lib.ptr(g), int(g.dtype == torch.bfloat16), e,
+                                       ctypes.byref(d), _lib.ptr(params[-1]), _lib.ptr(zsave),
+                                       _lib.ptr(feats), _lib.ptr(grad_h), _lib.ptr(part_h),
+                                       _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
+        small = part_h.sum(0)
+        grads, off = [], 0
+        for p in params[:-1]:
+            grads.append(small[off: off + p.numel()].view_as(p))
+            off += p.numel()
+        grads.append(part_wo.sum(0))
         return (None, None, *grads)
 
 

@@ -167,6 +167,35 @@ int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int 
                       int nodes_per_slice, float* partial, int n_partial, int w_total,
                       const eelg_linw_desc* desc, void* stream);
 
+/* Radial MLP of the interaction block, fused (gnn/blocks.py:537-549, applied at :590):
+ *   [Linear(n_feat -> hidden) + SiLU] + ([Linear(hidden -> hidden) + SiLU]) * (n_hidden - 1)
+ *   + Linear(hidden -> n_out, no bias)
+ * on edge features feats[E, n_feat], fp32 MFMA throughout.  Built for hidden 32 / 64,
+ * n_hidden 1..3, n_feat <= 32 (the reference default is 12 -> 64 -> 64 -> weight_numel).
+ * w / b: the hidden Linear weights [hidden, in] and biases [hidden] in torch layout.
+ * Forward: out[E, n_out] (fp32, or bf16 bit patterns when out_bf16) and the pre-activations
+ * zsave[n_hidden, E, hidden] (the backward's operand); wo_t = W_o^T [hidden, n_out]. */
+#define EELG_RADIAL_MAXH 3
+typedef struct {
+  int n_feat, hidden, n_hidden, n_out;
+  const float* w[EELG_RADIAL_MAXH];
+  const float* b[EELG_RADIAL_MAXH];
+} eelg_radial_desc;
+int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const float* wo_t,
+                    int out_bf16, float* zsave, void* out, void* stream);
+/* Partial-buffer sizes of eelg_radial_bwd for E edges: part_h has n_part rows of
+ * hidden*n_feat + hidden + (n_hidden-1)*(hidden^2 + hidden) floats (grad W_0, grad b_0, grad W_1,
+ * ... in torch layout); part_wo is [n_split, n_out, hidden]. */
+int eelg_radial_plan(int n_edges, int n_out, int* n_part, int* n_split);
+/* Backward from grad_w[E, n_out] (fp32, or bf16 when grad_bf16; wo = W_o [n_out, hidden]):
+ * per-wave / per-split partials of every weight and bias gradient; the caller sums part_h
+ * and part_wo over their first axis (deterministic).  grad_h[E, hidden] is workspace (it
+ * receives grad_w W_o).  No gradient w.r.t. feats (the reference's edge features carry
+ * none). */
+int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
+                    const float* wo, const float* zsave, const float* feats, float* grad_h,
+                    float* part_h, float* part_wo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
