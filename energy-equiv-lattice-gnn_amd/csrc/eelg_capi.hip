@@ -238,7 +238,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
-  info[5] = c.Dout;
+  info[5] = c.Dout; info[6] = c.nbc;
   *sig = c.sig;
   return 0;
 }
@@ -421,12 +421,14 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
                      float* partial, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
-  if (chunk <= 0 || chunk % c->nbc)
-    return fail(-2, "sc_bwd_coef: chunk must be a positive multiple of %d", c->nbc);
+  if (chunk != c->nbc)
+    return fail(-2, "sc_bwd_coef: chunk must be the config's coefficient chunk %d (info[6]), got %d",
+                c->nbc, chunk);
   if (n_nodes <= 0) return 0;
+  // one workgroup per (chunk of nbc LDS-resident nodes, channel)
   const int nch = (n_nodes + chunk - 1) / chunk;
-  hipLaunchKernelGGL(c->bwd_coef, dim3((c->njg + c->wpb - 1) / c->wpb, nch, mul), dim3(64 * c->wpb), 0,
-                     (hipStream_t)stream, xt, gt, n_nodes, chunk, partial);
+  hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul), dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,
+                     n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
 }
 

@@ -49,9 +49,14 @@ TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # 0.86): twice the VGPRs and LDS per workgroup halve the occupancy, the SGPR coefficient
 # operands need aligned pairs (s_mov per term), and dependent v_pk ops carry a wait state
 SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
-# coefficient gradient: 64-node sub-tiles per staged LDS tile
-SC_COEF_SUB = int(os.environ.get("EELG_SC_COEF_SUB", "4"))
-SC_COEF_NOUNROLL = int(os.environ.get("EELG_SC_COEF_NOUNROLL", "0"))
+# coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, sub-tile unroll
+SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
+SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
+SC_COEF_UNROLL = int(os.environ.get("EELG_SC_COEF_UNROLL", "1"))
+# nodes per lane per sweep step (2: operand pairs of adjacent nodes in one ds_read_b64, half the
+# LDS read cycles per node) and the most accumulators (terms) per wave
+SC_COEF_NPL = int(os.environ.get("EELG_SC_COEF_NPL", "1"))
+SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
 TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
 
 
@@ -943,69 +948,59 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         emit_cmajor(cmajor_out, lout)
 
     # ---------------- backward w.r.t. coefficients ----------------
-    JG = 64 if PKN == 1 else 32               # terms per wave (packed: 2 nodes per accumulator)
-    NSB = 64 * PKN                            # nodes per sub-tile (one lane each, or two packed)
-    NBC = NSB * SC_COEF_SUB                   # nodes per staged tile (one barrier pair)
-    WPB = 8                                   # waves (term groups) per workgroup
+    # grad coef[c, t] = sum_n g_q(n) x_a(n) x_b(n) x_c(n).  A workgroup owns one channel and
+    # one chunk of SC_COEF_CHUNK nodes: it stages the chunk's channel-major x / g rows into LDS
+    # ONCE (every byte of xt / gt crosses HBM once per launch), then its SC_COEF_WAVES waves
+    # sweep the staged chunk once per term group (JG accumulators per lane, one lane per node
+    # of a 64-node sub-tile) with no further barrier.  The per-lane sums are reduced over the
+    # 64 lanes by recursive halving (eelg_lane_reduce64), so lane t ends with term t of the
+    # group.  Deterministic partials part[chunk, c, t], summed over chunks by the caller.
+    assert PKN == 1, "packed fp32 coefficient gradient is not generated"
+    NCB = SC_COEF_CHUNK
+    WV = SC_COEF_WAVES
+    NPL = SC_COEF_NPL
+    gpw = -(-nt // (WV * SC_COEF_MAXJG))      # term groups per wave
+    JG = -(-nt // (WV * gpw))                 # terms per group (<= 64)
+    assert JG <= 64 and NCB % (64 * NPL) == 0 and NPL in (1, 2)
     groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
-    L.append(f"// coefficient gradient from channel-major x / g: {len(groups)} term groups of <= {JG};")
-    L.append(f"// a workgroup = one channel x {WPB} term groups (waves) sharing staged 64-node tiles;")
-    L.append("// per-lane partial sums over the chunk, then a recursive-halving lane reduction.")
-    L.append(f"__global__ __launch_bounds__({64 * WPB}) void sc_bwd_coef_{name}(")
+    nsub = NCB // (64 * NPL)
+    NC4 = NCB // 4
+    L.append(f"// coefficient gradient: {len(groups)} term groups of <= {JG} terms, {gpw} per wave;")
+    L.append(f"// one workgroup = one channel x {NCB} LDS-resident nodes")
+    L.append(f"__global__ __launch_bounds__({64 * WV}) void sc_bwd_coef_{name}(")
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
-    L.append(f"  __shared__ float sx[{D} * {NBC}];")
-    L.append(f"  __shared__ float sg[{Dout} * {NBC}];")
-    L.append("  const int c = blockIdx.z;")
+    L.append(f"  __shared__ float sx[{D} * {NCB}];")
+    L.append(f"  __shared__ float sg[{Dout} * {NCB}];")
+    L.append("  const int ch = blockIdx.x, c = blockIdx.y;")
+    L.append(f"  const int nb = ch * {NCB};")
+    L.append(f"  const int cnt = min({NCB}, n_nodes - nb);")
+    L.append("  const bool vec = (n_nodes & 3) == 0;")
+    L.append(f"  for (int i = threadIdx.x; i < {(D + Dout) * NC4}; i += {64 * WV}) {{")
+    L.append(f"    const int a = i / {NC4}, j = 4 * (i - a * {NC4});")
+    L.append(f"    const float* __restrict__ src = a < {D} ? xt + ((size_t)c * {D} + a) * n_nodes"
+             f" : gt + ((size_t)c * {Dout} + (a - {D})) * n_nodes;")
+    L.append(f"    float* __restrict__ sdst = a < {D} ? sx + a * {NCB} + j : sg + (a - {D}) * {NCB} + j;")
+    L.append("    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);")
+    L.append("    if (vec && j + 4 <= cnt) {")
+    L.append("      v = *reinterpret_cast<const float4*>(src + nb + j);")
+    L.append("    } else {")
+    L.append("      if (j + 0 < cnt) v.x = src[nb + j + 0];")
+    L.append("      if (j + 1 < cnt) v.y = src[nb + j + 1];")
+    L.append("      if (j + 2 < cnt) v.z = src[nb + j + 2];")
+    L.append("      if (j + 3 < cnt) v.w = src[nb + j + 3];")
+    L.append("    }")
+    L.append("    *reinterpret_cast<float4*>(sdst) = v;")
+    L.append("  }")
+    L.append("  __syncthreads();")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
-    L.append(f"  const int jg = __builtin_amdgcn_readfirstlane(blockIdx.x * {WPB} + wv);")
-    L.append(f"  const float* __restrict__ xs = xt + (size_t)c * {D} * n_nodes;")
-    L.append(f"  const float* __restrict__ gs = gt + (size_t)c * {Dout} * n_nodes;")
-    L.append("  const int nb = blockIdx.y * chunk;")
-    L.append("  const int ne = min(n_nodes, nb + chunk);")
-    L.append(f"  {FT} acc[{JG}];")
+    L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {nt};")
+    L.append(f"  for (int k = 0; k < {gpw}; ++k) {{")
+    L.append(f"    const int jg = __builtin_amdgcn_readfirstlane(k * {WV} + wv);")
+    L.append("    float acc[64];")
     L.append("#pragma unroll")
-    L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = {ZERO};")
-    # double-buffered staging: the next tile's global loads are in flight (in
-    # registers) while the current tile is consumed from LDS
-    per = (max(D, Dout) * NBC + 64 * WPB - 1) // (64 * WPB)
-    for it in range(per):
-        L.append(f"  float rx{it} = 0.0f, rg{it} = 0.0f;")
-
-    def issue(base):
-        out = []
-        for it in range(per):
-            out.append(f"    {{ const int idx = threadIdx.x + {64 * WPB * it}; const int a = idx >> {NBC.bit_length() - 1}, n = {base} + (idx & {NBC - 1});")
-            out.append(f"      rx{it} = (idx < {D * NBC} && n < ne) ? xs[(size_t)a * n_nodes + n] : 0.0f;"
-                       f" rg{it} = (idx < {Dout * NBC} && n < ne) ? gs[(size_t)a * n_nodes + n] : 0.0f; }}")
-        return out
-    L += issue("nb")
-
-    def tile_loop(body):
-        """the 64-node tile loop; every wave of the workgroup runs it (same barrier count)"""
-        out = [f"      for (int n0 = nb; n0 < ne; n0 += {NBC}) {{"]
-        for it in range(per):
-            out.append(f"        {{ const int idx = threadIdx.x + {64 * WPB * it}; if (idx < {D * NBC}) sx[idx] = rx{it};"
-                       f" if (idx < {Dout * NBC}) sg[idx] = rg{it}; }}")
-        out.append("        __syncthreads();")
-        out.append(f"        if (n0 + {NBC} < ne) {{")
-        out += ["    " + ln for ln in issue(f"n0 + {NBC}")]
-        out.append("        }")
-        if body:
-            # the wave sweeps the staged tile's sub-tiles with the same accumulators: more
-            # independent work per barrier pair
-            if SC_COEF_NOUNROLL:
-                out.append("#pragma unroll 1")
-            out.append(f"        for (int sb = 0; sb < {SC_COEF_SUB}; ++sb) {{")
-            out += body
-            out.append("        }")
-        out.append("        __syncthreads();")
-        out.append("      }")
-        return out
-
-    # each case owns its tile loop, so the 64 accumulators stay in place across tiles
-    # (a switch inside the loop merges them every iteration: 64 v_mov per tile)
-    L.append("  switch (jg) {")
+    L.append("    for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
+    L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
         L.append(f"    case {gi}: {{")
         need_x, need_g = set(), set()
@@ -1017,68 +1012,53 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 need_x.add(b)
             if nu >= 3:
                 need_x.add(cc)
-        body = []
-        # packed: a lane owns the adjacent nodes 2 * lane, 2 * lane + 1 of the tile (ds_read_b64)
-        for a in sorted(need_x):
-            body.append(f"        const {FT} x{a} = *reinterpret_cast<const {FT}*>(&sx[{a * NBC} + sb * {NSB} + {PKN} * lane]);")
-        for q in sorted(need_g):
-            body.append(f"        const {FT} g{q} = *reinterpret_cast<const {FT}*>(&sg[{q * NBC} + sb * {NSB} + {PKN} * lane]);")
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
-        cur = None
-        for jj, t in enumerate(grp):
-            nu, (a, b, cc), q = plan.terms[t]
-            if nu == 1:
-                body.append(f"        acc[{jj}] = {fma_v(f'x{a}', f'g{q}', f'acc[{jj}]')};")
-                continue
-            if cur != (a, b):
-                if cur is not None:
-                    body.append("        }")
-                    body.append("        " + cpin)
-                body.append(f"        {{ const {FT} p = x{a} * x{b};")
-                cur = (a, b)
-            if nu == 2:
-                body.append(f"          acc[{jj}] = {fma_v('p', f'g{q}', f'acc[{jj}]')};")
-            else:
-                body.append(f"          acc[{jj}] = {fma_v(f'p * x{cc}', f'g{q}', f'acc[{jj}]')};")
-        if cur is not None:
-            body.append("        }")
-        body.append("        " + cpin)
-        L += tile_loop(body)
+        L.append(f"#pragma unroll {SC_COEF_UNROLL}")
+        L.append(f"      for (int sb = 0; sb < {nsub}; ++sb) {{")
+        L.append(f"        const int o = sb * {64 * NPL} + {NPL} * lane;")
+        if NPL == 1:
+            for a in sorted(need_x):
+                L.append(f"        const float x{a} = sx[{a * NCB} + o];")
+            for q in sorted(need_g):
+                L.append(f"        const float g{q} = sg[{q * NCB} + o];")
+            halves = [""]
+        else:
+            # adjacent nodes o, o + 1 of one operand in one 8-byte read; the terms run per node
+            for a in sorted(need_x):
+                L.append(f"        const float2 x{a} = *reinterpret_cast<const float2*>(&sx[{a * NCB} + o]);")
+            for q in sorted(need_g):
+                L.append(f"        const float2 g{q} = *reinterpret_cast<const float2*>(&sg[{q * NCB} + o]);")
+            halves = [".x", ".y"]
+        for h in halves:
+            cur = None
+            for jj, t in enumerate(grp):
+                nu, (a, b, cc), q = plan.terms[t]
+                if nu == 1:
+                    L.append(f"        acc[{jj}] = fmaf(x{a}{h}, g{q}{h}, acc[{jj}]);")
+                    continue
+                if cur != (a, b):
+                    if cur is not None:
+                        L.append("        }")
+                        L.append("        " + cpin)
+                    L.append(f"        {{ const float p = x{a}{h} * x{b}{h};")
+                    cur = (a, b)
+                if nu == 2:
+                    L.append(f"          acc[{jj}] = fmaf(p, g{q}{h}, acc[{jj}]);")
+                else:
+                    L.append(f"          acc[{jj}] = fmaf(p * x{cc}{h}, g{q}{h}, acc[{jj}]);")
+            if cur is not None:
+                L.append("        }")
+            L.append("        " + cpin)
+        L.append("      }")
         L.append("      break; }")
-    L.append("    default: {")
-    L += tile_loop([])
-    L.append("      break; }")
-    L.append("  }")
-    # recursive-halving reduction over the lane bits: each step trades half of the values
-    # with the partner lane (bit b), so after log2(JG) steps (bits 32, 16, ...) lane L holds
-    # term L >> (6 - log2(JG)); the remaining low lane bits are summed by butterflies
-    k = JG.bit_length() - 1
-    assert 1 << k == JG and k <= 6
-    red = "acc" if PKN == 1 else "red"
-    if PKN == 2:
-        L.append(f"  float red[{JG}];")
-        L.append(f"  for (int i = 0; i < {JG}; ++i) red[i] = acc[i].x + acc[i].y;")
-    n = JG
-    bits = [32, 16, 8, 4, 2, 1]
-    for bit in bits[:k]:
-        h = n // 2
-        L.append(f"  {{ const bool up = (lane & {bit}) != 0;")
-        for i in range(h):
-            L.append(f"    {{ const float keep = up ? {red}[{i + h}] : {red}[{i}]; "
-                     f"const float give = up ? {red}[{i}] : {red}[{i + h}]; "
-                     f"{red}[{i}] = keep + __shfl_xor(give, {bit}); }}")
-            if i % 8 == 7:
-                L.append("    " + pin([f"{red}[{t}]" for t in range(i - 7, i + 1)], memory=False))
-        L.append("  }")
-        n = h
-    for bit in bits[k:]:
-        L.append(f"  {red}[0] += __shfl_xor({red}[0], {bit});")
-    low = (1 << (6 - k)) - 1
-    L.append(f"  if (jg < {len(groups)} && (lane & {low}) == 0) {{")
-    L.append(f"    float* __restrict__ dst = part + ((size_t)blockIdx.y * {MUL} + c) * {nt};")
-    L.append(f"    const int t = jg * {JG} + (lane >> {6 - k}); if (t < {nt}) dst[t] = {red}[0];")
+    L.append("    default: break;")
+    L.append("    }")
+    L.append("    eelg_lane_reduce64(acc);")
+    L.append(f"    const int t = jg * {JG} + lane;")
+    L.append(f"    if (jg < {len(groups)} && lane < {JG} && t < {nt}) dst[t] = acc[0];")
     L.append("  }")
     L.append("}")
+    WPB, NBC = WV, NCB
     info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info

@@ -339,7 +339,7 @@ class _SymCon(torch.autograd.Function):
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
                                               _lib.stream(gt)), "sc_cmajor")
                 TIMER.stop(tok)
-            chunk = max(256, min(4096, (n // 16 + 255) // 256 * 256))   # a multiple of the tile
+            chunk = ctx.info["coef_chunk"]          # LDS-resident nodes per workgroup
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
             side = ctx.side

@@ -36,11 +36,12 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out} (D: coupling components
- * per channel of the input, D_out: of the output; they differ when the product maps the
- * SH-lmax interaction irreps onto wider hidden irreps) */
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk} (D: coupling
+ * components per channel of the input, D_out: of the output; they differ when the product maps
+ * the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node chunk of
+ * eelg_sc_bwd_coef) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info6, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info7, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -137,10 +138,11 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
  * which = 0: input (coupling) layout, 1: output layout. */
 int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
                    void* stream);
-/* Coefficient gradient from channel-major x and grad_out:
- * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk) (chunk % 256 == 0 is
- * always accepted; the generated tile may allow smaller multiples);
- * the caller sums over chunks (deterministic). */
+/* Coefficient gradient from channel-major x and grad_out (replaces the weight gradient
+ * through the U.W contraction of gnn/mace.py:242-277):
+ * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk); chunk must be the
+ * config's coef_chunk (eelg_sc_info info[6]): one workgroup keeps that many nodes of one
+ * channel resident in LDS.  The caller sums over chunks (deterministic). */
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* grad_out_t, int n_nodes, int mul,
                      int chunk, float* partial, void* stream);
 

@@ -330,3 +330,42 @@ def test_stream_overlap_matches_in_line_bitwise():
     assert torch.equal(outs[0][0], outs[1][0])
     for g0, g1 in zip(outs[0][1], outs[1][1]):
         assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("lmax,n", [(4, 1), (4, 300), (4, 513), (4, 2051), (3, 1027)])
+def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
+    """eelg_sc_bwd_coef over several LDS-resident node chunks (a ragged last chunk, n not a
+    multiple of 4) against the fp64 sum over nodes of g_q x_a x_b x_c per polynomial term
+    (SURVEY 8c per-kernel tolerance 1e-5, reduction order only).  The partial buffer starts
+    as NaN, so a chunk or term the kernel skips fails the test."""
+    from gnn import _lib, cg
+    from gnn.mace import SymmetricContraction
+    hid = "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
+    sc = SymmetricContraction(hid, hid, 3).to(DEV)
+    idx, info = sc._config()
+    plan = cg.symcon_plan("+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)),
+                          tuple(range(lmax + 1)), 3)
+    D, Do, nt, chunk = info["D"], info["Dout"], info["nterms"], info["coef_chunk"]
+    assert len(plan.terms) == nt
+    torch.manual_seed(n)
+    xt = torch.randn(32 * D, n, device=DEV)
+    gt = torch.randn(32 * Do, n, device=DEV)
+    nch = -(-n // chunk)
+    part = torch.full((nch, 32, nt), float("nan"), device=DEV)
+    lib = _lib.load()
+    _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(xt), _lib.ptr(gt), n, 32, chunk, _lib.ptr(part),
+                                    _lib.stream(part)), "sc_bwd_coef")
+    got = part.sum(0)
+    # wrong chunk sizes are rejected, not silently mis-tiled
+    with pytest.raises(_lib.EELGError):
+        _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(xt), _lib.ptr(gt), n, 32, chunk * 2,
+                                        _lib.ptr(part), _lib.stream(part)), "sc_bwd_coef")
+    A = torch.tensor([a for _, (a, b, c), q in plan.terms], device=DEV)
+    B = torch.tensor([b if b >= 0 else D for _, (a, b, c), q in plan.terms], device=DEV)
+    C = torch.tensor([c if c >= 0 else D for _, (a, b, c), q in plan.terms], device=DEV)
+    Q = torch.tensor([q for _, (a, b, c), q in plan.terms], device=DEV)
+    X = torch.cat([xt.view(32, D, n).double(), torch.ones(32, 1, n, device=DEV, dtype=torch.float64)], 1)
+    G = gt.view(32, Do, n).double()
+    want = torch.stack([(X[c, A] * X[c, B] * X[c, C] * G[c, Q]).sum(-1) for c in range(32)])
+    assert torch.isfinite(got).all()
+    assert rel_err(got, want) < 1e-5

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Build a kernel variant of libeelg.so into variants/libeelg_<tag>.so with generator env overrides.
-# usage: EELG_TP_NPH=8 EELG_TP_MAXACC=24 tools/build_variant.sh <tag>
+# Build a kernel variant of libeelg.so into variants/libeelg_<tag>.so with generator env overrides
+# (EELG_* knobs of csrc/gen_kernels.py) and optional EXTRA hipcc flags, through the same Makefile.
+# usage: EELG_SC_COEF_UNROLL=2 tools/build_variant.sh <tag>     (load it with EELG_LIB=...)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=/tmp/eelg_var_$1
@@ -8,9 +9,6 @@ rm -rf "$T"; mkdir -p "$T/a/p" "$R/variants"
 cp -r "$R/energy-equiv-lattice-gnn_amd/csrc" "$T/a/p/csrc"
 cp -r "$R/energy-equiv-lattice-gnn_amd/gnn" "$T/a/p/gnn"
 cp -r "$R/include" "$T/a/include"
-cd "$T/a/p/csrc"
-python3 gen_kernels.py generated > /dev/null
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -mcode-object-version=5 -fno-gpu-rdc -fno-slp-vectorize \
-  -Wno-unused-variable -Wno-unused-result $EXTRA_FLAGS -Rpass-analysis=kernel-resource-usage \
-  -o "$R/variants/libeelg_$1.so" eelg_capi.hip > "$T/ru.log" 2>&1
-grep -A7 "Name: _Z13tp_fwd_tpB_l4" "$T/ru.log" | grep -E "VGPRs:|Spill|Occupancy" | sed "s/^/$1 /"
+rm -rf "$T/a/p/csrc/build" "$T/a/p/csrc/generated"
+make -s -C "$T/a/p/csrc" OUT="$R/variants/libeelg_$1.so" > "$T/build.log" 2>&1 || { tail -20 "$T/build.log"; exit 1; }
+echo "built variants/libeelg_$1.so"

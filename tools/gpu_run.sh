@@ -1,6 +1,7 @@
 #!/bin/bash
 # Generic GPU-box step runner: gpu_run.sh <tag> <test-selector> [extra python script args...]
-#   runs `pytest -m gpu <selector>` (if not "-"), then each remaining argument as a python
+#   runs `pytest -m gpu <selector>` (if not "-"; env K = a pytest -k expression), then each
+#   remaining argument as a python
 #   command line (quoted), each under its own time limit, writing under gpurun_out/<tag>/.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -10,7 +11,7 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 cd "$R"
 if [ "$SEL" != "-" ]; then
-  timeout -k 10 900 python -u -m pytest $SEL -m gpu -v -x --timeout 400 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $SEL ${K:+-k "$K"} -m gpu -v -x --timeout 400 --timeout-method thread \
       > "$O/tests.log" 2>&1 || { echo "tests rc=$?" >> "$O/tests.log"; exit 3; }
 fi
 i=0

@@ -134,7 +134,7 @@ def main():
     rec("sc_cmajor", timeit_if("sc_cmajor", cm, args.reps), 4 * 2 * n * 800)
     cm()
     ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream(x)), "cm")
-    chunk = max(256, min(4096, (n // 16 + 255) // 256 * 256))    # as gnn/ops.py
+    chunk = sinfo["coef_chunk"]                                     # as gnn/ops.py
     nch = (n + chunk - 1) // chunk
     part = torch.empty(nch, 32, nt, device=dev)
 
