@@ -445,6 +445,20 @@ int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias
     if (sl.bias_off >= 0 && sl.d != 1) return fail(-2, "linear_fwd: bias on a non-scalar slot");
   }
   if (n_nodes <= 0) return 0;
+  if (lin_fwd_fast_ok(x, x_row, y, y_row, desc)) {
+    // groups of 32/d whole nodes; the d = 9 slots have the most (ceil(n / 3))
+    int max_groups = 0;
+    for (int s = 0; s < desc->n_slots; ++s) {
+      const int nb = 32 / desc->slot[s].d;
+      const int g = (n_nodes + nb - 1) / nb;
+      max_groups = g > max_groups ? g : max_groups;
+    }
+    const int gblocks = (max_groups + LINF_WAVES * LINF_GPW - 1) / (LINF_WAVES * LINF_GPW);
+    dim3 grid(((gblocks + 7) / 8) * 8 * desc->max_jt, desc->n_slots, 1);
+    hipLaunchKernelGGL(lin_fwd_fast_kernel, grid, dim3(64 * LINF_WAVES), 0, (hipStream_t)stream, x,
+                       x_row, w, bias, n_nodes, y, y_row, *desc);
+    return check_launch("linear_fwd");
+  }
   dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, 1);  // column tiles loop in-kernel
   hipLaunchKernelGGL(lin_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, w, bias,
                      n_nodes, y, y_row, *desc);
@@ -467,8 +481,12 @@ int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int 
   const int slices = (n_nodes + nodes_per_slice - 1) / nodes_per_slice;
   if (n_partial < slices) return fail(-2, "linear_bwd_w: partial has %d rows, need %d", n_partial, slices);
   dim3 grid(slices, desc->n_ins, desc->max_ut * desc->max_jt);
-  hipLaunchKernelGGL(lin_bwdw_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g, g_row,
-                     n_nodes, nodes_per_slice, partial, w_total, *desc);
+  if (lin_bwdw_fast_ok(x, x_row, g, g_row, desc))
+    hipLaunchKernelGGL(lin_bwdw_fast_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g,
+                       g_row, n_nodes, nodes_per_slice, partial, w_total, *desc);
+  else
+    hipLaunchKernelGGL(lin_bwdw_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g, g_row,
+                       n_nodes, nodes_per_slice, partial, w_total, *desc);
   return check_launch("linear_bwd_w");
 }
 

@@ -252,6 +252,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
 // chunks of floor(32/d) whole nodes round-robin, stage their X[row][u] / G[row][j] tiles
 // (node-contiguous 32*d-float runs) in wave-private LDS, reduce over rows with MFMA
 // (zero-padded to 32 rows), and the four accumulators are summed through LDS at the end.
+// Fast path of grad W (full 32x32 tiles, 16-B aligned rows): each wave stages chunks of
+// NB = floor(32/D) whole nodes in their natural global layout -- per node the u-tile's 32*D
+// floats of x, then the j-tile's 32*D floats of g, both contiguous runs -- with float4 loads and
+// ds_write_b128 (no transposition, conflict-free).  The MFMA K axis runs over the chunk's
+// (node, m) rows: row r = (n, m) sits at n*32*D + m, and lane u reads x[r][u] at + u*D, an odd
+// stride (D = 2l+1) over the 32 banks, so the operand reads are conflict-free too.  Rows past
+// NB*D point at a zeroed node region.  Same partial layout as the general path.
+template <int D>
+__device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x_row,
+                                              const float* __restrict__ g, int g_row, int n0,
+                                              int n1, const eelg_linw_ins& in, int ut, int jt,
+                                              float* __restrict__ xw, float* __restrict__ gw,
+                                              eelg_f32x16& acc) {
+  constexpr int NB = 32 / D;            // whole nodes per chunk
+  constexpr int RUN4 = 8 * D;           // float4 per node run (32 * D floats)
+  constexpr int NQ = (NB * RUN4 + 63) / 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, u = lane & 31, hf = lane >> 5;
+  // zero node region (rows >= NB*D)
+  for (int f = lane; f < 32 * D; f += 64) {
+    xw[NB * 32 * D + f] = 0.0f;
+    gw[NB * 32 * D + f] = 0.0f;
+  }
+  int off[16];
+#pragma unroll
+  for (int st = 0; st < 16; ++st) {
+    const int r = 2 * st + hf;
+    off[st] = (r < NB * D ? (r / D) * 32 * D + (r % D) : NB * 32 * D) + u * D;
+  }
+  const float* __restrict__ xb = x + in.x_off + (size_t)ut * 32 * D;
+  const float* __restrict__ gb = g + in.g_off + (size_t)jt * 32 * D;
+  float4 rx[NQ], rg[NQ];
+  auto load_chunk = [&](int nc) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int f = lane + 64 * q;
+      const int a = f / RUN4, w4 = f - a * RUN4;
+      const bool ok = f < NB * RUN4 && nc + a < n1;
+      const int nn = ok ? nc + a : 0;
+      rx[q] = ok ? *reinterpret_cast<const float4*>(xb + (size_t)nn * x_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rg[q] = ok ? *reinterpret_cast<const float4*>(gb + (size_t)nn * g_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  int nc = n0 + wave * NB;
+  if (nc < n1) load_chunk(nc);
+  for (; nc < n1; nc += 4 * NB) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int f = lane + 64 * q;
+      if (f < NB * RUN4) {
+        reinterpret_cast<float4*>(xw)[f] = rx[q];
+        reinterpret_cast<float4*>(gw)[f] = rg[q];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (nc + 4 * NB < n1) load_chunk(nc + 4 * NB);
+#pragma unroll
+    for (int st = 0; st < 16; ++st)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[off[st]], gw[off[st]], acc, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 #ifndef LIN_BWDW_WPE
 #define LIN_BWDW_WPE 2
 #endif
@@ -276,14 +338,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_BWDW_WP
   const int nb = 32 / d;  // whole nodes per chunk
   float* __restrict__ xs = Xs[wave];
   float* __restrict__ gs = Gs[wave];
+  eelg_f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
   // pad rows [nb*d, 32) stay zero for the whole kernel
   for (int f = lane; f < (32 - nb * d) * LIN_ST; f += 64) {
     xs[nb * d * LIN_ST + f] = 0.0f;
     gs[nb * d * LIN_ST + f] = 0.0f;
   }
-  eelg_f32x16 acc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
   const float* __restrict__ xb = x + in.x_off + (size_t)ut * 32 * d;
   const float* __restrict__ gb = g + in.g_off + (size_t)jt * 32 * d;
   // register-staged chunk: lane owns flat entries f = lane + 64 q (q < 16) of the
@@ -346,4 +408,243 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_BWDW_WP
       if (uu < K && j < NO) dst[(size_t)uu * NO + j] = v * in.alpha;
     }
   }
+}
+
+// grad W, every instruction on the fast path (lin_bwdw_fast): same grid and partial layout as
+// lin_bwdw_kernel, no register-staged transposition, so the register budget allows 4 waves/SIMD
+__global__ __launch_bounds__(256) void lin_bwdw_fast_kernel(const float* __restrict__ x, int x_row,
+                                                            const float* __restrict__ g, int g_row,
+                                                            int n_nodes, int nodes_per_slice,
+                                                            float* __restrict__ partial, int w_total,
+                                                            eelg_linw_desc desc) {
+  __shared__ float4 lds4[2 * 4 * 1152 / 4];   // per wave (32/D + 1) * 32 * D floats of x and g
+  const eelg_linw_ins& in = desc.ins[blockIdx.y];
+  const int d = in.d, K = in.k, NO = in.n_out;
+  const int n_jt = NO / 32;
+  const int t = blockIdx.z;
+  if (t >= (K / 32) * n_jt) return;  // uniform per workgroup
+  const int ut = t / n_jt, jt = t - ut * n_jt;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int slice = blockIdx.x;
+  const int n0 = slice * nodes_per_slice;
+  const int n1 = min(n_nodes, n0 + nodes_per_slice);
+  eelg_f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  float* xw = reinterpret_cast<float*>(lds4) + wave * 2 * 1152;
+  float* gwv = xw + 1152;
+  switch (d) {
+    case 1: lin_bwdw_fast<1>(x, x_row, g, g_row, n0, n1, in, ut, jt, xw, gwv, acc); break;
+    case 3: lin_bwdw_fast<3>(x, x_row, g, g_row, n0, n1, in, ut, jt, xw, gwv, acc); break;
+    case 5: lin_bwdw_fast<5>(x, x_row, g, g_row, n0, n1, in, ut, jt, xw, gwv, acc); break;
+    case 7: lin_bwdw_fast<7>(x, x_row, g, g_row, n0, n1, in, ut, jt, xw, gwv, acc); break;
+    default: lin_bwdw_fast<9>(x, x_row, g, g_row, n0, n1, in, ut, jt, xw, gwv, acc); break;
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds4);
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[((wave - 1) * 16 + i) * 64 + lane] = acc[i];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* __restrict__ dst = partial + (size_t)slice * w_total + in.w_off;
+    const int j = jt * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[i] + red[i * 64 + lane] + red[(16 + i) * 64 + lane] + red[(32 + i) * 64 + lane];
+      const int uu = ut * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      dst[(size_t)uu * NO + j] = v * in.alpha;
+    }
+  }
+}
+
+// whether every instruction of a grad-W descriptor qualifies for lin_bwdw_fast_kernel
+static bool lin_bwdw_fast_ok(const float* x, int x_row, const float* g, int g_row,
+                             const eelg_linw_desc* desc) {
+  if ((x_row & 3) || (g_row & 3) || (reinterpret_cast<uintptr_t>(x) & 15) ||
+      (reinterpret_cast<uintptr_t>(g) & 15))
+    return false;
+  for (int t = 0; t < desc->n_ins; ++t) {
+    const eelg_linw_ins& in = desc->ins[t];
+    if (in.k % 32 || in.n_out % 32 || (in.x_off & 3) || (in.g_off & 3)) return false;
+    if (in.d != 1 && in.d != 3 && in.d != 5 && in.d != 7 && in.d != 9) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward / grad-x fast path (every slot: whole 32-wide K chunks and column tiles, d odd <= 9,
+// 16-B aligned input rows).  A workgroup (8 waves) owns one output slot, one 32-column tile and
+// LINF_GPW node groups per wave; it stages the slot's weight tile (all sources, alpha applied)
+// in LDS once.  A wave owns groups of NB = floor(32/D) whole nodes and stages each 32-wide K
+// chunk of their rows in the natural global layout (per node the chunk's 32*D floats, one
+// contiguous run: float4 loads, ds_write_b128), with node stride SX = 32*D + pad chosen so the
+// MFMA operand reads -- lane i = row (n, m) at n*SX + m + k*D -- spread over the banks
+// (at most 2-way; 4-way for D = 1).  No workgroup barrier after the weight staging.
+// ---------------------------------------------------------------------------------------------
+#define LINF_WAVES 8
+#define LINF_GPW 4
+#define LINF_KMAX 320          // sum of the slot's source K held in LDS
+#define LINF_XW 1152           // per-wave X region (floats) >= NB * SX for every D
+
+template <int D>
+struct LinfGeom {
+  static constexpr int NB = 32 / D;
+  static constexpr int SX = 32 * D + (D >= 7 ? 8 : 4);
+  static constexpr int RUN4 = 8 * D;                       // float4 per node per K chunk
+  static constexpr int NQ = (NB * RUN4 + 63) / 64;          // float4 loads per lane per chunk
+};
+
+template <int D>
+__device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
+                                             const float* __restrict__ bias, int n_nodes,
+                                             float* __restrict__ y, int y_row,
+                                             const eelg_lin_slot& sl, int gb, int jt,
+                                             const float* __restrict__ ws, float* __restrict__ xw) {
+  using G = LinfGeom<D>;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
+  const int n_groups = (n_nodes + G::NB - 1) / G::NB;
+  const int g_base = gb * LINF_WAVES * LINF_GPW;
+  int nch = 0;
+  for (int s = 0; s < sl.n_src; ++s) nch += sl.src[s].k / 32;
+  int my_groups = 0;
+  for (int k = 0; k < LINF_GPW; ++k) my_groups += (g_base + k * LINF_WAVES + wave < n_groups);
+  const int nq = my_groups * nch;
+  if (nq == 0) return;
+  // this lane's operand row
+  const bool row_ok = i < G::NB * D;
+  const int abase = (i / D) * G::SX + (i % D) + hf * D;
+  const int bbase = hf * 32 + i;
+  const float bj = (sl.bias_off >= 0 && D == 1) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
+  float4 r[G::NQ];
+  auto chunk_of = [&](int q, int& group, int& xoff, int& kb) {
+    const int k = q / nch;
+    int c = q - k * nch;
+    group = g_base + k * LINF_WAVES + wave;
+    int s = 0;
+    kb = 0;
+    while (c >= sl.src[s].k / 32) { c -= sl.src[s].k / 32; kb += sl.src[s].k; ++s; }
+    xoff = sl.src[s].x_off + c * 32 * D;
+    kb += c * 32;
+  };
+  auto load = [&](int q) {
+    int group, xoff, kb;
+    chunk_of(q, group, xoff, kb);
+    const int n0 = group * G::NB;
+#pragma unroll
+    for (int qq = 0; qq < G::NQ; ++qq) {
+      const int f = lane + 64 * qq;
+      const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+      const bool ok = f < G::NB * G::RUN4 && n0 + a < n_nodes;
+      r[qq] = ok ? *reinterpret_cast<const float4*>(x + (size_t)(n0 + a) * x_row + xoff + 4 * w4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  eelg_f32x16 acc;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = bj;
+  load(0);
+  for (int q = 0; q < nq; ++q) {
+    int group, xoff, kb;
+    chunk_of(q, group, xoff, kb);
+#pragma unroll
+    for (int qq = 0; qq < G::NQ; ++qq) {
+      const int f = lane + 64 * qq;
+      if (f < G::NB * G::RUN4) {
+        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+        *reinterpret_cast<float4*>(xw + a * G::SX + 4 * w4) = r[qq];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (q + 1 < nq) load(q + 1);
+    const float* __restrict__ wk = ws + kb * 32 + bbase;
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float av = xw[abase + 2 * st * D];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(row_ok ? av : 0.0f, wk[2 * st * 32], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if ((q + 1) % nch == 0) {
+      // epilogue of the group: acc[t] = (row (t&3) + 8(t>>2) + 4hf, column i) goes through the
+      // wave's LDS region in the output's natural layout (per node the tile's 32*D floats), then
+      // out as float4 runs
+      const int n0 = group * G::NB;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int row = (t & 3) + 8 * (t >> 2) + 4 * hf;
+        const int n = row / D, m = row - (row / D) * D;
+        if (row < G::NB * D) xw[n * G::SX + i * D + m] = acc[t];
+        acc[t] = bj;
+      }
+      __builtin_amdgcn_wave_barrier();
+      float* __restrict__ yb = y + sl.y_off + (size_t)jt * 32 * D;
+#pragma unroll
+      for (int qq = 0; qq < G::NQ; ++qq) {
+        const int f = lane + 64 * qq;
+        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+        if (f < G::NB * G::RUN4 && n0 + a < n_nodes)
+          *reinterpret_cast<float4*>(yb + (size_t)(n0 + a) * y_row + 4 * w4) =
+              *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
+    const float* __restrict__ x, int x_row, const float* __restrict__ w,
+    const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
+    eelg_lin_desc desc) {
+  __shared__ float ws[LINF_KMAX * 32];
+  __shared__ float4 xw4[LINF_WAVES * LINF_XW / 4];
+  const eelg_lin_slot& sl = desc.slot[blockIdx.y];
+  // block id -> (group block gb, column tile jt): the max_jt column-tile blocks of one group
+  // block are dispatched back to back on one XCD (id % 8), so the rows they all read come
+  // from HBM once and from that XCD's L2 after
+  const int id = blockIdx.x, xcd = id & 7, rest = id >> 3;
+  const int jt = rest % desc.max_jt, gb = (rest / desc.max_jt) * 8 + xcd;
+  const int d = sl.d;
+  if (jt * 32 >= sl.n_out) return;
+  const int nb = 32 / d;
+  const int n_groups = (n_nodes + nb - 1) / nb;
+  if (gb * LINF_WAVES * LINF_GPW >= n_groups) return;   // uniform per workgroup
+  // weight tile: ws[kb + k][j] = alpha_s * W_s[k][jt*32 + j] over the slot's sources
+  int kb = 0;
+  for (int s = 0; s < sl.n_src; ++s) {
+    const eelg_lin_src& src = sl.src[s];
+    for (int e = threadIdx.x; e < src.k * 32; e += 64 * LINF_WAVES) {
+      const int k = e >> 5, jj = e & 31;
+      ws[(kb + k) * 32 + jj] = w[src.w_off + (size_t)k * src.ldk + (size_t)(jt * 32 + jj) * src.ldj] * src.alpha;
+    }
+    kb += src.k;
+  }
+  __syncthreads();
+  float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
+  switch (d) {
+    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+  }
+}
+
+static bool lin_fwd_fast_ok(const float* x, int x_row, const float* y, int y_row,
+                            const eelg_lin_desc* desc) {
+  if ((x_row & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (y_row & 3) ||
+      (reinterpret_cast<uintptr_t>(y) & 15))
+    return false;
+  for (int s = 0; s < desc->n_slots; ++s) {
+    const eelg_lin_slot& sl = desc->slot[s];
+    if (sl.n_out % 32 || (sl.y_off & 3)) return false;
+    if (sl.d != 1 && sl.d != 3 && sl.d != 5 && sl.d != 7 && sl.d != 9) return false;
+    int kt = 0;
+    for (int t = 0; t < sl.n_src; ++t) {
+      if (sl.src[t].k % 32 || (sl.src[t].x_off & 3)) return false;
+      kt += sl.src[t].k;
+    }
+    if (kt > LINF_KMAX) return false;
+  }
+  return true;
 }

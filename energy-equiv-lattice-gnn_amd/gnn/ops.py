@@ -53,6 +53,8 @@ TIMER = KernelTimer()
 # chain and its gradient); EELG_OVERLAP=0 runs everything in line on the current stream
 OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
 SC_CMAJOR_ON_SIDE = os.environ.get("EELG_SC_CMAJOR_SIDE", "0") != "0"   # measured equal; fused keeps fewer bytes
+# the contraction's coefficient gradient on the coefficient side stream (1) or in line (0)
+SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
@@ -342,7 +344,7 @@ class _SymCon(torch.autograd.Function):
             chunk = ctx.info["coef_chunk"]          # LDS-resident nodes per workgroup
             nch = (n + chunk - 1) // chunk
             part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
-            side = ctx.side
+            side = ctx.side if (SC_COEF_ON_SIDE or cm_side) else None
             if side is not None:
                 # the coefficient gradient runs on the side stream, where its consumer (the
                 # coefficient chain's backward) runs too; the main stream goes on meanwhile
