@@ -483,8 +483,15 @@ static bool lin_bwdw_fast_ok(const float* x, int x_row, const float* g, int g_ro
 // MFMA operand reads -- lane i = row (n, m) at n*SX + m + k*D -- spread over the banks
 // (at most 2-way; 4-way for D = 1).  No workgroup barrier after the weight staging.
 // ---------------------------------------------------------------------------------------------
+#ifndef LINF_WAVES
 #define LINF_WAVES 8
+#endif
+#ifndef LINF_GPW
 #define LINF_GPW 4
+#endif
+#ifndef LINF_PFD
+#define LINF_PFD 1             // K chunks in flight per wave (1 or 2; 2 measured no faster)
+#endif
 #define LINF_KMAX 320          // sum of the slot's source K held in LDS
 #define LINF_XW 1152           // per-wave X region (floats) >= NB * SX for every D
 
@@ -517,7 +524,6 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   const int abase = (i / D) * G::SX + (i % D) + hf * D;
   const int bbase = hf * 32 + i;
   const float bj = (sl.bias_off >= 0 && D == 1) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
-  float4 r[G::NQ];
   auto chunk_of = [&](int q, int& group, int& xoff, int& kb) {
     const int k = q / nch;
     int c = q - k * nch;
@@ -528,7 +534,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
     xoff = sl.src[s].x_off + c * 32 * D;
     kb += c * 32;
   };
-  auto load = [&](int q) {
+  auto load = [&](int q, float4* r) {
     int group, xoff, kb;
     chunk_of(q, group, xoff, kb);
     const int n0 = group * G::NB;
@@ -544,8 +550,8 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   eelg_f32x16 acc;
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = bj;
-  load(0);
-  for (int q = 0; q < nq; ++q) {
+  // one pipeline step: chunk q (registers r) to LDS, chunk q + LINF_PFD's loads into r, MFMAs
+  auto step = [&](int q, float4* r) {
     int group, xoff, kb;
     chunk_of(q, group, xoff, kb);
 #pragma unroll
@@ -557,7 +563,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       }
     }
     __builtin_amdgcn_wave_barrier();
-    if (q + 1 < nq) load(q + 1);
+    if (q + LINF_PFD < nq) load(q + LINF_PFD, r);
     const float* __restrict__ wk = ws + kb * 32 + bbase;
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
@@ -589,6 +595,18 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       }
       __builtin_amdgcn_wave_barrier();
     }
+  };
+  // LINF_PFD chunks in flight per wave: register sets used round-robin (static indexing)
+  float4 ra[G::NQ], rb[G::NQ];
+  load(0, ra);
+  if (LINF_PFD == 2 && nq > 1) load(1, rb);
+  if (LINF_PFD == 2) {
+    for (int q = 0; q < nq; q += 2) {
+      step(q, ra);
+      if (q + 1 < nq) step(q + 1, rb);
+    }
+  } else {
+    for (int q = 0; q < nq; ++q) step(q, ra);
   }
 }
 
@@ -598,7 +616,8 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
     eelg_lin_desc desc) {
   __shared__ float ws[LINF_KMAX * 32];
   __shared__ float4 xw4[LINF_WAVES * LINF_XW / 4];
-  const eelg_lin_slot& sl = desc.slot[blockIdx.y];
+  // the last slots (highest l, the most rows) are dispatched first: a shorter tail
+  const eelg_lin_slot& sl = desc.slot[desc.n_slots - 1 - blockIdx.y];
   // block id -> (group block gb, column tile jt): the max_jt column-tile blocks of one group
   // block are dispatched back to back on one XCD (id % 8), so the rows they all read come
   // from HBM once and from that XCD's L2 after
