@@ -53,8 +53,12 @@ __global__ __launch_bounds__(256) void edge_embed_kernel(
   const int nsh = (lmax + 1) * (lmax + 1);
   const int nshp = (nsh + 3) & ~3;   // rows padded to 16 B: the TP kernels read them as float4
   float* __restrict__ she = sh + (size_t)e * nshp;
-  if (lmax == 4) sh_eval_l4(vx, vy, vz, she);
-  else sh_eval_l3(vx, vy, vz, she);
+  switch (lmax) {
+    case 1: sh_eval_l1(vx, vy, vz, she); break;
+    case 2: sh_eval_l2(vx, vy, vz, she); break;
+    case 3: sh_eval_l3(vx, vy, vz, she); break;
+    default: sh_eval_l4(vx, vy, vz, she); break;
+  }
   for (int j = nsh; j < nshp; ++j) she[j] = 0.0f;
   // soft_one_hot_linspace(x, 0, end, nb, 'gaussian', cutoff=False):
   // values = linspace(0, end, nb); step = values[1]-values[0]; exp(-((x-v)/step)^2)/1.12
@@ -246,7 +250,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
 int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, const float* shifts,
                     const float* radius, int n_edges, int lmax, int nb, float len_end,
                     float rad_end, float* sh, float* feats, void* stream) {
-  if (lmax != 3 && lmax != 4) return fail(-2, "edge_embed: lmax %d not built (3 or 4)", lmax);
+  if (lmax < 1 || lmax > 4) return fail(-2, "edge_embed: lmax %d not built (1..4)", lmax);
   if (nb < 2) return fail(-2, "edge_embed: need >= 2 bases, got %d", nb);
   if (n_edges <= 0) return 0;
   hipLaunchKernelGGL(edge_embed_kernel, dim3((n_edges + 255) / 256), dim3(256), 0,

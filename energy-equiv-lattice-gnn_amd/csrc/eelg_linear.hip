@@ -656,7 +656,7 @@ static bool lin_fwd_fast_ok(const float* x, int x_row, const float* y, int y_row
     return false;
   for (int s = 0; s < desc->n_slots; ++s) {
     const eelg_lin_slot& sl = desc->slot[s];
-    if (sl.n_out % 32 || (sl.y_off & 3)) return false;
+    if (sl.n_out % 32 || (sl.y_off & 3) || sl.n_src == 0) return false;   // sourceless: general path writes zeros
     if (sl.d != 1 && sl.d != 3 && sl.d != 5 && sl.d != 7 && sl.d != 9) return false;
     int kt = 0;
     for (int t = 0; t < sl.n_src; ++t) {

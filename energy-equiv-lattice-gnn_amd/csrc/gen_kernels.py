@@ -29,10 +29,10 @@ from typing import Sequence, Dict, List, Tuple
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-from gnn import cg  # noqa: E402
+from gnn import cg, kernel_sets  # noqa: E402
 from gnn.irreps import Ir, Irreps  # noqa: E402
 
-MUL = 32
+MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
@@ -78,25 +78,26 @@ def hidden_irreps(lmax: int, mul: int = MUL) -> Irreps:
 
 
 def tp_configs() -> Dict[str, Tuple[Irreps, Irreps, Irreps]]:
+    """gnn/kernel_sets.py: node irreps 32x0e (tpA) or the hidden irreps (tpB) x SH(lmax)."""
     out = {}
-    for lmax in (3, 4):
+    for lmax in kernel_sets.LMAX:
         sh = Irreps.spherical_harmonics(lmax)
         target = (sh * MUL).sort()[0].simplify()
+        assert str(target) == kernel_sets.coupling_target(lmax)
         out[f"tpA_l{lmax}"] = (Irreps(f"{MUL}x0e"), sh, target)
         out[f"tpB_l{lmax}"] = (hidden_irreps(lmax), sh, target)
     return out
 
 
 def sc_configs() -> Dict[str, Tuple[str, Tuple[int, ...], int]]:
-    """coupling = the interaction irreps (SH lmax), outputs = the hidden irreps.  Hidden
-    irreps beyond the SH lmax are not generated: the reference's U_matrix_real fails for
-    them (an output irrep with no degree-1 path leaves ``last_ir`` unbound,
-    gnn/mace.py:466-476)."""
+    """coupling = the interaction irreps (SH lmax), outputs = the hidden irreps, correlation
+    1..3 (gnn/kernel_sets.py).  Hidden irreps beyond the SH lmax are not generated: the
+    reference's U_matrix_real fails for them (an output irrep with no degree-1 path leaves
+    ``last_ir`` unbound, gnn/mace.py:466-476)."""
     out = {}
-    for lmax, hmax in ((3, 3), (4, 4)):
-        coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
-        key = f"sc_l{lmax}_c3" if hmax == lmax else f"sc_l{lmax}h{hmax}_c3"
-        out[key] = (coupling, tuple(range(hmax + 1)), 3)
+    for lmax in kernel_sets.LMAX:
+        for corr in kernel_sets.CORRELATIONS:
+            out[f"sc_l{lmax}_c{corr}"] = (kernel_sets.coupling_str(lmax), tuple(range(lmax + 1)), corr)
     return out
 
 
@@ -1080,7 +1081,7 @@ def main(outdir: str) -> None:
              " return __builtin_elementwise_fma(a, b, c); }",
              "__device__ __forceinline__ eelg_f2 eelg_fma2s(float a, eelg_f2 b, eelg_f2 c) {"
              " return __builtin_elementwise_fma(eelg_f2{a, a}, b, c); }", ""]
-    for lmax in (3, 4):
+    for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     tp_table, sc_table = [], []
     for name, (node, sh, target) in tp_configs().items():

@@ -20,7 +20,7 @@ from typing import Optional, Tuple, Union
 import numpy as np
 import torch
 
-from . import _lib, cg, ops
+from . import _lib, cg, kernel_sets, ops
 from .irreps import Irreps
 from .mace import SymmetricContraction
 from .o3 import Gate, Linear, TensorProduct
@@ -169,6 +169,8 @@ class TensorProductInteractionBlock(torch.nn.Module):
         if self.reduce != "sum":
             raise NotImplementedError("only interaction_reduction='sum' is on the hot path "
                                       "(the PNA branch is out of scope, SURVEY.md section 2)")
+        # fail at construction, with the supported list, for structures without generated kernels
+        kernel_sets.check_tp(self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
         self.linear_up = Linear(self._node_feats_irreps, self._node_feats_irreps)
         irreps_mid, instructions = cg.tp_out_irreps_with_instructions(
             self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)

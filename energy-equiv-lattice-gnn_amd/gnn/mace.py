@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, cg, ops
+from . import _lib, cg, kernel_sets, ops
 from .irreps import Ir, Irreps
 
 tp_out_irreps_with_instructions = cg.tp_out_irreps_with_instructions
@@ -45,18 +45,16 @@ class SymmetricContraction(torch.nn.Module):
         coupling = "+".join(str(ir) for _, ir in self.irreps_in)
         lmax = self.irreps_in.lmax
         ls = tuple(ir.l for _, ir in self.irreps_out)
-        expect = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
-        if (coupling != expect or correlation != 3 or self.mul != 32
-                or any(m != self.mul for m, _ in self.irreps_in)
-                or any(m != self.mul or ir.p != (-1) ** ir.l for m, ir in self.irreps_out)):
-            raise NotImplementedError(
-                f"symmetric contraction kernels are generated for 32x(0e..{lmax}) inputs, 32x "
-                f"natural-parity outputs, correlation 3; got {self.irreps_in} -> {self.irreps_out}, "
-                f"correlation {correlation}")
         if any(ir.l > lmax for _, ir in self.irreps_out):
             raise NotImplementedError(
                 f"output irreps {self.irreps_out} beyond the coupling lmax {lmax}: the reference "
                 "U_matrix_real has no degree-1 path for them (gnn/mace.py:466-476)")
+        if any(m != self.mul or ir.p != (-1) ** ir.l for m, ir in self.irreps_out):
+            raise NotImplementedError(
+                f"symmetric contraction outputs {self.irreps_out}: the kernels are generated for "
+                f"{self.mul}x natural-parity outputs")
+        # fail at construction, with the supported list, for structures without generated kernels
+        kernel_sets.check_sc(self.irreps_in, tuple(ir.l for _, ir in self.irreps_out), correlation)
         plan = cg.symcon_plan(coupling, ls, correlation)
         self._sig = cg.fnv1a64(cg.sc_signature(coupling, ls, correlation))
         self.block_order = [(l, nu) for l, nu, _ in plan.weight_blocks]

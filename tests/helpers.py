@@ -41,3 +41,20 @@ def batch_to(b, device, dtype=None):
         for k in ("positions", "node_attrs", "shifts", "edge_attr", "stiffness"):
             setattr(out, k, getattr(out, k).to(dtype))
     return out
+
+
+def record_parity(key: str, **vals) -> None:
+    """Append measured parity errors to the JSON file named by EELG_PARITY_OUT (if set):
+    the GPU runs keep the achieved error next to each stated tolerance."""
+    import json
+    import os
+    out = os.environ.get("EELG_PARITY_OUT")
+    if not out:
+        return
+    data = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            data = json.load(f)
+    data[key] = vals
+    with open(out, "w") as f:
+        json.dump(data, f, indent=1)

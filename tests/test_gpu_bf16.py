@@ -6,14 +6,14 @@ Tolerances (stated per test):
   to bf16 -> 2^-8 relative per element; grad_x sums bf16-rounded per-edge terms -> 1e-2;
 * end to end vs the fp64 oracle (SURVEY.md section 8c, bf16 variant): stiffness and loss
   2e-2 relative; parameter gradients: all gradients together 2e-2 relative to their max, and
-  every parameter's gradient at cosine similarity >= 0.99 with the oracle's (a per-parameter
+  every parameter's gradient at cosine similarity >= 0.999 with the oracle's (a per-parameter
   max-relative bound is meaningless for parameters whose gradient is ~1e-3 of the others',
   e.g. layer 0's 3o contraction weights, where bf16 noise of the large terms dominates).
 """
 import pytest
 import torch
 
-from helpers import batch, batch_to, copy_params, params
+from helpers import batch, batch_to, copy_params, params, record_parity
 
 import oracle.model as omodel
 from oracle.train import stiffness_loss as oracle_loss
@@ -106,11 +106,15 @@ def test_model_bf16_storage_matches_oracle(lmax):
     gm = torch.cat([pm.grad.double().cpu().reshape(-1) for _, pm in m.named_parameters()])
     go = torch.cat([po[n].grad.reshape(-1) for n in names])
     assert rel_err(gm, go) < 2e-2
+    cos_min = 1.0
     for name, pm in m.named_parameters():
         a, r = pm.grad.double().cpu().reshape(-1), po[name].grad.reshape(-1)
         if float(r.norm()) == 0.0:          # structurally unused output (e.g. the last layer's 1o)
             assert float(a.abs().max()) <= 1e-6 * float(go.abs().max()), name
             continue
         cos = float(a @ r / (a.norm() * r.norm()).clamp_min(1e-300))
-        assert cos >= 0.99, (name, cos)
+        cos_min = min(cos_min, cos)
+        assert cos >= 0.999, (name, cos)
+    record_parity(f"bf16_model_l{lmax}", stiffness=rel_err(cm, co),
+                  grad_all=rel_err(gm, go), cos_min=cos_min)
 

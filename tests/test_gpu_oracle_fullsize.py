@@ -1,7 +1,7 @@
 """The HIP path against the fp64 CPU oracle at BASELINE's own graph sizes.
 
 * config 2 (``BASELINE.json`` configs[1]): one 1024-node / 4096-edge lattice, 4 layers,
-  lmax 4, fp32 -- stiffness and loss within 1e-4, every parameter gradient within 1e-4 of
+  lmax 4, fp32 -- stiffness and loss within 1e-4, every parameter gradient within 2e-5 of
   its own largest entry (the small-graph tests allow 1e-3);
 * config 5 (configs[4]): one 5000-node / 20000-edge lattice, 4 layers, lmax 3, bf16
   storage of the edge-sized tensors with fp32 arithmetic -- stiffness and loss within 2e-2
@@ -25,7 +25,7 @@ import oracle.mace as omace
 import oracle.model as omodel
 from oracle.train import stiffness_loss as oracle_loss
 
-from helpers import batch_to, copy_params, params
+from helpers import batch_to, copy_params, params, record_parity
 from helpers_mandel import rotate_mandel
 
 pytestmark = pytest.mark.gpu
@@ -40,10 +40,7 @@ def rel_err(a, b):
 
 def _record(key, **vals):
     MEASURED[key] = vals
-    out = os.environ.get("EELG_PARITY_OUT")
-    if out:
-        with open(out, "w") as f:
-            json.dump(MEASURED, f, indent=1)
+    record_parity(key, **vals)
 
 
 def _one_graph(n_nodes, n_edges, lmax, storage):
@@ -96,7 +93,7 @@ def test_config2_graph_matches_fp64_oracle():
     _record("config2_1x1024", **r)
     assert r["stiffness"] < 1e-4, r
     assert r["loss"] < 1e-4, r
-    assert r["grad_worst"] < 1e-4, r
+    assert r["grad_worst"] < 2e-5, r
 
 
 def test_config5_graph_matches_fp64_oracle():

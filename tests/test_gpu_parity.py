@@ -1,15 +1,16 @@
 """HIP hot path vs the CPU oracle (float64) on identical inputs.
 
 Tolerances (fp32 device arithmetic vs fp64 oracle), stated per test:
-* kernel level: max |dev - ref| <= 2e-5 * max|ref| (+ tiny atol)
-* end to end (stiffness, loss, gradients): <= 1e-4 * max|ref|
+* kernel / block level (SURVEY 8c per-kernel rtol): max |dev - ref| <= 1e-5 * max|ref|
+* end to end: stiffness and loss <= 1e-4 * max|ref|, every parameter gradient
+  <= 1e-5 of its own largest entry (measured <= 2.3e-6, gpurun_out parity records)
 """
 import math
 
 import pytest
 import torch
 
-from helpers import batch, batch_to, copy_params, params
+from helpers import batch, batch_to, copy_params, params, record_parity
 
 import oracle.blocks as ob
 import oracle.mace as omace
@@ -143,11 +144,14 @@ def test_interaction_block_fwd_bwd(layer_index):
     xm = x.float().to(DEV).requires_grad_(True)
     ym, _ = m_int(xm, sh.float().to(DEV), ef.float().to(DEV), bd.edge_index)
     (ym * go.float().to(DEV)).sum().backward()
-    assert rel_err(ym, yo) < 2e-5
-    assert rel_err(xm.grad, xo.grad) < 2e-5
     po = dict(o_int.named_parameters())
-    for name, pm in m_int.named_parameters():
-        assert rel_err(pm.grad, po[name].grad) < 5e-5, name
+    gerr = {name: rel_err(pm.grad, po[name].grad) for name, pm in m_int.named_parameters()}
+    record_parity(f"interaction_block_l{layer_index}", out=rel_err(ym, yo), grad_x=rel_err(xm.grad, xo.grad),
+                  grad_params=max(gerr.values()))
+    assert rel_err(ym, yo) < 1e-5
+    assert rel_err(xm.grad, xo.grad) < 1e-5
+    for name, e in gerr.items():
+        assert e < 1e-5, name
 
 
 def test_product_block_fwd_bwd():
@@ -163,20 +167,27 @@ def test_product_block_fwd_bwd():
     xm = x.float().to(DEV).requires_grad_(True)
     ym = m_p(xm, None)
     (ym * go.float().to(DEV)).sum().backward()
-    assert rel_err(ym, yo) < 2e-5
-    assert rel_err(xm.grad, xo.grad) < 2e-5
     po = dict(o_p.named_parameters())
-    for name, pm in m_p.named_parameters():
-        assert rel_err(pm.grad, po[name].grad) < 5e-5, name
+    gerr = {name: rel_err(pm.grad, po[name].grad) for name, pm in m_p.named_parameters()}
+    record_parity("product_block", out=rel_err(ym, yo), grad_x=rel_err(xm.grad, xo.grad),
+                  grad_params=max(gerr.values()))
+    assert rel_err(ym, yo) < 1e-5
+    assert rel_err(xm.grad, xo.grad) < 1e-5
+    for name, e in gerr.items():
+        assert e < 1e-5, name
 
 
-@pytest.mark.parametrize("message_passes,lmax", [(2, 4), (4, 4), (2, 3)])
-def test_model_forward_backward_matches_oracle(message_passes, lmax):
-    """lmax 3 = BASELINE config 5's irreps (SH and hidden irreps up to l = 3)."""
+@pytest.mark.parametrize("message_passes,lmax,correlation",
+                         [(2, 4, 3), (4, 4, 3), (2, 3, 3), (2, 2, 3), (2, 1, 3), (2, 4, 2), (2, 4, 1),
+                          (2, 3, 2), (2, 2, 1)])
+def test_model_forward_backward_matches_oracle(message_passes, lmax, correlation):
+    """Every generated kernel family (gnn/kernel_sets.py): SH / hidden lmax 1..4 and
+    correlation 1..3; lmax 3 = BASELINE config 5's irreps.  Stiffness and loss within 1e-4,
+    every parameter gradient within 1e-5 of its own largest entry."""
     from gnn.model import EnergyEquivGNN
     from gnn.train import stiffness_loss
     b, bd, csr, rmax = _setup()
-    p = params(message_passes, lmax=lmax, max_edge_radius=rmax)
+    p = params(message_passes, lmax=lmax, max_edge_radius=rmax, correlation=correlation)
     torch.manual_seed(0)
     o = omodel.EnergyEquivGNN(p).double()
     m = EnergyEquivGNN(p).to(DEV)
@@ -188,11 +199,13 @@ def test_model_forward_backward_matches_oracle(message_passes, lmax):
     cm = m(bd)["stiffness"]
     lm = stiffness_loss(cm, bd.stiffness)
     lm.backward()
-    assert rel_err(cm, co) < 1e-4
-    assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
     po = dict(o.named_parameters())
     worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
-    assert worst < 1e-3
+    record_parity(f"model_mp{message_passes}_l{lmax}_c{correlation}", stiffness=rel_err(cm, co),
+                  loss=abs(lm.item() - lo.item()) / abs(lo.item()), grad_params=worst)
+    assert rel_err(cm, co) < 1e-4
+    assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
+    assert worst < 1e-5
 
 
 def test_model_rotation_equivariance_and_psd():

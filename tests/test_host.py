@@ -134,24 +134,49 @@ def test_library_loads_and_exports_every_header_symbol():
 
 
 def test_library_config_tables_match_host_structure():
-    from gnn import _lib
-    for lmax in (3, 4):
+    """Every kernel set gnn/kernel_sets.py lists is in the library under its name, with the
+    structure hash the host derives (lmax 1..4, correlation 1..3)."""
+    from gnn import _lib, kernel_sets
+    for lmax in kernel_sets.LMAX:
         sh = Irreps.spherical_harmonics(lmax)
         target = (sh * 32).sort()[0].simplify()
-        hid = Irreps("+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+        hid = Irreps(kernel_sets.hidden_irreps_str(lmax))
         for name, node in ((f"tpA_l{lmax}", Irreps("32x0e")), (f"tpB_l{lmax}", hid)):
             _, info, sig = _lib.tp_config(name)
             paths = cg.tp_paths(node, sh, target)
             assert info["din"] == node.dim and info["npaths"] == len(paths)
             assert info["wn"] == 32 * len(paths) and info["nsh"] == sh.dim
             assert sig == cg.fnv1a64(cg.tp_signature(node, sh, target))
-        coupling = "+".join(f"{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
-        _, info, sig = _lib.sc_config(f"sc_l{lmax}_c3")
-        plan = cg.symcon_plan(coupling, tuple(range(lmax + 1)), 3)
-        assert info["nterms"] == len(plan.terms) and info["x_row"] == 32 * plan.D
-        assert sig == cg.fnv1a64(cg.sc_signature(coupling, tuple(range(lmax + 1)), 3))
+        coupling = kernel_sets.coupling_str(lmax)
+        for corr in kernel_sets.CORRELATIONS:
+            _, info, sig = _lib.sc_config(f"sc_l{lmax}_c{corr}")
+            plan = cg.symcon_plan(coupling, tuple(range(lmax + 1)), corr)
+            assert info["nterms"] == len(plan.terms) and info["x_row"] == 32 * plan.D
+            assert sig == cg.fnv1a64(cg.sc_signature(coupling, tuple(range(lmax + 1)), corr))
     with pytest.raises(_lib.EELGError):
         _lib.tp_config("no_such_config")
+
+
+def test_unsupported_params_fail_at_construction_with_the_supported_list():
+    """params whose irreps structure has no generated kernels raise when the model is built
+    (not at the first forward), naming the generated sets (gnn/kernel_sets.py)."""
+    from argparse import Namespace
+    from helpers import params
+    from gnn.model import EnergyEquivGNN
+    for change in (dict(lmax=5, hidden_irreps="32x0e+32x1o+32x2e+32x3o+32x4e+32x5o"),
+                   dict(hidden_irreps="64x0e+64x1o+64x2e+64x3o+64x4e"),
+                   dict(hidden_irreps="32x0e+32x1o+32x2e"),
+                   dict(correlation=4)):
+        p = Namespace(**{**vars(params(2)), **change})
+        with pytest.raises(NotImplementedError, match="generated kernel sets"):
+            EnergyEquivGNN(p)
+    for lmax in (1, 2, 3, 4):
+        for corr in (1, 2, 3):
+            from gnn import kernel_sets
+            p = Namespace(**{**vars(params(2)), "lmax": lmax, "correlation": corr,
+                             "hidden_irreps": kernel_sets.hidden_irreps_str(lmax),
+                             "readout_irreps": kernel_sets.hidden_irreps_str(lmax, 16)})
+            EnergyEquivGNN(p)
 
 
 def test_product_rejects_cpu_tensors_loudly():
@@ -191,13 +216,6 @@ def test_radial_mlp_is_hip_only_and_checks_shapes():
             TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=dim,
                                           MLP_layers=layers)
     TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=32, MLP_layers=4)
-
-
-def test_wgrad_split_k_matches_matmul():
-    from gnn.ops import _wgrad
-    g = torch.randn(1300, 8, dtype=torch.float64)
-    x = torch.randn(1300, 5, dtype=torch.float64)
-    assert torch.allclose(_wgrad(g, x, chunk=256), g.t() @ x, atol=1e-10)
 
 
 def test_lmax3_with_l4_hidden_irreps_raises_like_the_reference():
