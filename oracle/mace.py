@@ -62,6 +62,20 @@ def get_edge_vectors_and_lengths(positions, edge_index, shifts, normalize=False,
 def _wigner_nj(irrepss, dtype=torch.float64):
     """``gnn/mace.py:363-432`` (normalization='component', no filter)."""
     irrepss = [Irreps(x) for x in irrepss]
+    names = {str(x) for x in irrepss}
+    if len(names) == 1 and dtype == torch.float64:
+        # n copies of one irreps (every U_matrix_real call): memoised per process, the
+        # result is shared by every output irrep and contraction of that coupling
+        return list(_wigner_nj_same(names.pop(), len(irrepss)))
+    return _wigner_nj_impl(irrepss, dtype)
+
+
+@functools.lru_cache(maxsize=None)
+def _wigner_nj_same(irreps: str, n: int):
+    return tuple(_wigner_nj_impl([Irreps(irreps)] * n, torch.float64))
+
+
+def _wigner_nj_impl(irrepss, dtype):
     if len(irrepss) == 1:
         (irreps,) = irrepss
         ret, e, i = [], torch.eye(irreps.dim, dtype=dtype), 0
