@@ -32,6 +32,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FETCH_CORRECTION = 2.0   # HBM read bytes per FETCH_SIZE byte on gfx950 (measured, any load width)
 
 
 def _free_port() -> int:
@@ -110,9 +111,15 @@ def pmc_traffic(kernel: str, args) -> dict | None:
     if not hits:
         return None
     t = max(hits, key=lambda v: sum(v.values()))
-    fetch, write = t.get("FETCH_SIZE", 0.0), t.get("WRITE_SIZE", 0.0)
+    fetch_raw, write = t.get("FETCH_SIZE", 0.0), t.get("WRITE_SIZE", 0.0)
+    # gfx950 calibration (profiles/r02_fetch_calibration.md, tools/proto/fetch_calib.hip): a
+    # kernel reading 1 GiB once reports FETCH_SIZE = 0.500 GiB at 4, 8, 12 and 16 B per lane;
+    # WRITE_SIZE reports 1.000 GiB for 1 GiB written.  HBM read bytes = 2 x FETCH_SIZE.
+    fetch = FETCH_CORRECTION * fetch_raw
     return {"bytes": round(fetch + write), "fetch": round(fetch), "write": round(write),
-            "source": f"profiles/pmc_traffic.json ({tab['source']})"}
+            "fetch_raw": round(fetch_raw), "fetch_correction": FETCH_CORRECTION,
+            "source": f"profiles/pmc_traffic.json ({tab['source']}), "
+                      "calibration profiles/r02_fetch_calibration.md"}
 
 
 def host_cpu() -> dict:
@@ -420,6 +427,9 @@ def main():
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum[key]["count"]}
             if roof["traffic_detail"]:
                 roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)
+                # measured HBM bytes over the SURVEY 8d algorithmic bytes (x is gathered once per
+                # in-edge, not once per node, so > 1 is expected for a gather)
+                roof["traffic_detail"]["ratio_to_algorithmic"] = round(roof["traffic"] / byts, 3)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax,

@@ -8,11 +8,11 @@ writes
   profiles/<tag>_summary.md         top kernels per step + bench line + PMC traffic table
   profiles/pmc_traffic.json         per-kernel mean FETCH_SIZE / WRITE_SIZE bytes per launch
 
-Counter units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  WRITE_SIZE is exact for
-our stores (tp_fwd writes N*7360*4 B and the counter reads exactly that); the gfx950 "FETCH
-halving" (MI355X_MICROARCH.md, HBM) applies to 16-B/lane streaming reads only -- our kernels
-read 4-B/lane rows, and the sc_cmajor transpose (reads x once, 104.9 MB) reports 1.2x its
-bytes, so FETCH_SIZE is used raw here (calibration recorded in the summary).
+Counter units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  gfx950 calibration
+(profiles/r02_fetch_calibration.md, tools/proto/fetch_calib.hip): reading 1 GiB once reports
+FETCH_SIZE = 0.5 GiB at every load width (4, 8, 12, 16 B per lane); writing 1 GiB reports
+WRITE_SIZE = 1.0 GiB.  pmc_traffic.json keeps the raw counters; the tables below and bench.py
+report HBM read bytes = 2 x FETCH_SIZE.
 """
 import csv
 import collections
@@ -56,12 +56,14 @@ def main(src, tag):
             d[(r["Kernel_Name"].split("(")[0], r["Grid_Size"])].append(float(r["Counter_Value"]) * 1024)
         for (k, g), v in d.items():
             traffic[f"{k}|{g}"][c] = sum(v) / len(v)
-    lines += ["", "## HBM traffic per launch (PMC, separate FETCH_SIZE / WRITE_SIZE passes, KiB x 1024)", "",
-              "| kernel | grid | FETCH MB | WRITE MB |", "|---|---|---|---|"]
+    lines += ["", "## HBM traffic per launch (PMC, separate FETCH_SIZE / WRITE_SIZE passes, KiB x 1024; "
+              "reads = 2 x FETCH_SIZE, gfx950 calibration)", "",
+              "| kernel | grid | FETCH_SIZE MB (raw) | HBM read MB | WRITE MB |", "|---|---|---|---|---|"]
     for key in sorted(traffic, key=lambda k: -sum(traffic[k].values()))[:20]:
         k, g = key.split("|")
         t = traffic[key]
-        lines.append(f"| `{k[:60]}` | {g} | {t.get('FETCH_SIZE', 0)/1e6:.1f} | {t.get('WRITE_SIZE', 0)/1e6:.1f} |")
+        lines.append(f"| `{k[:60]}` | {g} | {t.get('FETCH_SIZE', 0)/1e6:.1f} | {2 * t.get('FETCH_SIZE', 0)/1e6:.1f} | "
+                     f"{t.get('WRITE_SIZE', 0)/1e6:.1f} |")
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     json.dump({"source": tag, "unit": "bytes per launch", "kernels": traffic},
               open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
