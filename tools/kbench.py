@@ -27,6 +27,26 @@ from gnn.irreps import Irreps  # noqa: E402
 ONLY = None
 
 
+def _morton(d):
+    """the same lattice with its nodes renumbered along a Morton (Z-order) curve"""
+    import copy
+    pos = d.positions
+    lo, hi = pos.min(0).values, pos.max(0).values
+    q = ((pos - lo) / (hi - lo).clamp_min(1e-12) * 1023).long().clamp(0, 1023)
+    key = torch.zeros(pos.shape[0], dtype=torch.long)
+    for bit in range(10):
+        for ax in range(3):
+            key |= ((q[:, ax] >> bit) & 1) << (3 * bit + ax)
+    perm = torch.argsort(key)
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel())
+    e = copy.copy(d)
+    e.positions = pos[perm]
+    e.node_attrs = d.node_attrs[perm]
+    e.edge_index = inv[d.edge_index]
+    return e
+
+
 def timeit(fn, reps):
     if reps == 0:
         return float("nan")
@@ -48,10 +68,14 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--graphs", type=int, default=32)
     ap.add_argument("--only", default="", help="regex: time only matching ops")
+    ap.add_argument("--morton", action="store_true", help="renumber each graph's nodes in Morton order")
     args = ap.parse_args()
     dev = "cuda"
     ds = SyntheticLattices(args.graphs, 1024, 4096, 1234)
-    b = collate([ds[g] for g in range(args.graphs)]).to(dev)
+    graphs = [ds[g] for g in range(args.graphs)]
+    if args.morton:
+        graphs = [_morton(g) for g in graphs]
+    b = collate(graphs).to(dev)
     n = b.node_attrs.shape[0]
     csr = ops.EdgeCSR.build(b.edge_index, n)
     e = csr.num_edges
