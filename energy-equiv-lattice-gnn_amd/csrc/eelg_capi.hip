@@ -485,9 +485,12 @@ int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int 
   const int slices = (n_nodes + nodes_per_slice - 1) / nodes_per_slice;
   if (n_partial < slices) return fail(-2, "linear_bwd_w: partial has %d rows, need %d", n_partial, slices);
   dim3 grid(slices, desc->n_ins, desc->max_ut * desc->max_jt);
-  if (lin_bwdw_fast_ok(x, x_row, g, g_row, desc))
-    hipLaunchKernelGGL(lin_bwdw_fast_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g,
+  if (lin_bwdw_fast_ok(x, x_row, g, g_row, desc)) {
+    // 1-D over (slice, tile), XCD-grouped (see lin_bwdw_fast_kernel)
+    dim3 gf(((slices + 7) / 8) * 8 * desc->max_ut * desc->max_jt, desc->n_ins, 1);
+    hipLaunchKernelGGL(lin_bwdw_fast_kernel, gf, dim3(256), 0, (hipStream_t)stream, x, x_row, g,
                        g_row, n_nodes, nodes_per_slice, partial, w_total, *desc);
+  }
   else
     hipLaunchKernelGGL(lin_bwdw_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, g, g_row,
                        n_nodes, nodes_per_slice, partial, w_total, *desc);

@@ -421,12 +421,17 @@ __global__ __launch_bounds__(256) void lin_bwdw_fast_kernel(const float* __restr
   const eelg_linw_ins& in = desc.ins[blockIdx.y];
   const int d = in.d, K = in.k, NO = in.n_out;
   const int n_jt = NO / 32;
-  const int t = blockIdx.z;
+  // block id -> (slice, weight tile): the tiles of one node slice (which all read that slice's
+  // g rows, and each its own x columns) are dispatched back to back on one XCD (id % 8)
+  const int ntile = desc.max_ut * desc.max_jt;
+  const int id = blockIdx.x, xcd = id & 7, rest = id >> 3;
+  const int t = rest % ntile;
+  const int slice = (rest / ntile) * 8 + xcd;
   if (t >= (K / 32) * n_jt) return;  // uniform per workgroup
   const int ut = t / n_jt, jt = t - ut * n_jt;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int slice = blockIdx.x;
   const int n0 = slice * nodes_per_slice;
+  if (n0 >= n_nodes) return;
   const int n1 = min(n_nodes, n0 + nodes_per_slice);
   eelg_f32x16 acc;
 #pragma unroll
