@@ -242,7 +242,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
-  info[5] = c.Dout; info[6] = c.nbc;
+  info[5] = c.Dout; info[6] = c.nbc; info[7] = c.coef_mm;
   *sig = c.sig;
   return 0;
 }
@@ -429,9 +429,11 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
     return fail(-2, "sc_bwd_coef: chunk must be the config's coefficient chunk %d (info[6]), got %d",
                 c->nbc, chunk);
   if (n_nodes <= 0) return 0;
-  // one workgroup per (chunk of nbc LDS-resident nodes, channel)
+  // one workgroup per (chunk of nbc LDS-resident nodes, channel); mul-major operands: 1-D grid
+  // with the mul channel workgroups of a chunk back to back on one XCD
   const int nch = (n_nodes + chunk - 1) / chunk;
-  hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul), dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,
+  const dim3 grid = c->coef_mm ? dim3(((nch + 7) / 8) * 8 * mul) : dim3(nch, mul);
+  hipLaunchKernelGGL(c->bwd_coef, grid, dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,
                      n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
 }

@@ -42,6 +42,7 @@ struct eelg_sc_cfg {
   eelg_sc_cmajor_fn cmajor_out;  // output layout
   int nb;                        // nodes per fwd / grad-x workgroup
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
+  int coef_mm;                   // 1: coef-grad reads mul-major x / grad_out (1-D XCD-grouped grid)
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

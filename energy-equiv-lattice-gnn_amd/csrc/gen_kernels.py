@@ -57,6 +57,10 @@ SC_COEF_UNROLL = int(os.environ.get("EELG_SC_COEF_UNROLL", "1"))
 # LDS read cycles per node) and the most accumulators (terms) per wave
 SC_COEF_NPL = int(os.environ.get("EELG_SC_COEF_NPL", "1"))
 SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
+# 1: the coefficient gradient reads the mul-major x / grad_out rows itself (no channel-major
+# copies; grad-x 0.73 -> 0.57 ms but coef-grad 0.51 -> 0.58 ms, and the step measured 0.7 %
+# slower, r02t); 0: it reads channel-major copies written by sc_bwd_x
+SC_COEF_MULMAJOR = int(os.environ.get("EELG_SC_COEF_MULMAJOR", "0"))
 TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
 
 
@@ -971,28 +975,56 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"__global__ __launch_bounds__({64 * WV}) void sc_bwd_coef_{name}(")
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
-    L.append(f"  __shared__ float sx[{D} * {NCB}];")
-    L.append(f"  __shared__ float sg[{Dout} * {NCB}];")
-    L.append("  const int ch = blockIdx.x, c = blockIdx.y;")
-    L.append(f"  const int nb = ch * {NCB};")
-    L.append(f"  const int cnt = min({NCB}, n_nodes - nb);")
-    L.append("  const bool vec = (n_nodes & 3) == 0;")
-    L.append(f"  for (int i = threadIdx.x; i < {(D + Dout) * NC4}; i += {64 * WV}) {{")
-    L.append(f"    const int a = i / {NC4}, j = 4 * (i - a * {NC4});")
-    L.append(f"    const float* __restrict__ src = a < {D} ? xt + ((size_t)c * {D} + a) * n_nodes"
-             f" : gt + ((size_t)c * {Dout} + (a - {D})) * n_nodes;")
-    L.append(f"    float* __restrict__ sdst = a < {D} ? sx + a * {NCB} + j : sg + (a - {D}) * {NCB} + j;")
-    L.append("    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);")
-    L.append("    if (vec && j + 4 <= cnt) {")
-    L.append("      v = *reinterpret_cast<const float4*>(src + nb + j);")
-    L.append("    } else {")
-    L.append("      if (j + 0 < cnt) v.x = src[nb + j + 0];")
-    L.append("      if (j + 1 < cnt) v.y = src[nb + j + 1];")
-    L.append("      if (j + 2 < cnt) v.z = src[nb + j + 2];")
-    L.append("      if (j + 3 < cnt) v.w = src[nb + j + 3];")
-    L.append("    }")
-    L.append("    *reinterpret_cast<float4*>(sdst) = v;")
-    L.append("  }")
+    if SC_COEF_MULMAJOR:
+        # operands read straight from the mul-major rows x[N, drow] / grad_out[N, orow] (no
+        # channel-major copies): the MUL channel workgroups of one chunk are dispatched back to
+        # back on one XCD (block id % 8), so the chunk's rows (NCB x (drow + orow) floats) are
+        # fetched from HBM once and served to the 32 channels from that XCD's L2
+        SXS = NCB + 1                          # odd stride: the staging stores spread over banks
+        lays = [(lin, "xt", drow), (lout, "gt", orow)]
+        offs = [lay.comp[a][2] for lay, _, _ in lays for a in range(lay.D)]
+        dims = [2 * lay.comp[a][0] + 1 for lay, _, _ in lays for a in range(lay.D)]
+        ms = [lay.comp[a][1] for lay, _, _ in lays for a in range(lay.D)]
+        L.append(f"  __shared__ float sx[{D} * {SXS}];")
+        L.append(f"  __shared__ float sg[{Dout} * {SXS}];")
+        L.append("  const int id = blockIdx.x, xcd = id & 7, rest = id >> 3;")
+        L.append(f"  const int c = rest % {MUL}, ch = (rest / {MUL}) * 8 + xcd;")
+        L.append(f"  const int nb = ch * {NCB};")
+        L.append("  if (nb >= n_nodes) return;   // uniform per workgroup")
+        L.append(f"  const int koff[{D + Dout}] = {{{', '.join(str(o + m) for o, m in zip(offs, ms))}}};")
+        L.append(f"  const int kd[{D + Dout}] = {{{', '.join(str(d) for d in dims)}}};")
+        L.append(f"  for (int i = threadIdx.x; i < {(D + Dout) * NCB}; i += {64 * WV}) {{")
+        L.append(f"    const int j = i / {D + Dout}, a = i - j * {D + Dout};")
+        L.append("    const int n = nb + j;")
+        L.append(f"    const bool isx = a < {D};")
+        L.append(f"    const float* __restrict__ row = isx ? xt + (size_t)n * {drow} : gt + (size_t)n * {orow};")
+        L.append("    const float v = n < n_nodes ? row[koff[a] + c * kd[a]] : 0.0f;")
+        L.append(f"    (isx ? sx + a * {SXS} : sg + (a - {D}) * {SXS})[j] = v;")
+        L.append("  }")
+    else:
+        SXS = NCB
+        L.append(f"  __shared__ float sx[{D} * {NCB}];")
+        L.append(f"  __shared__ float sg[{Dout} * {NCB}];")
+        L.append("  const int ch = blockIdx.x, c = blockIdx.y;")
+        L.append(f"  const int nb = ch * {NCB};")
+        L.append(f"  const int cnt = min({NCB}, n_nodes - nb);")
+        L.append("  const bool vec = (n_nodes & 3) == 0;")
+        L.append(f"  for (int i = threadIdx.x; i < {(D + Dout) * NC4}; i += {64 * WV}) {{")
+        L.append(f"    const int a = i / {NC4}, j = 4 * (i - a * {NC4});")
+        L.append(f"    const float* __restrict__ src = a < {D} ? xt + ((size_t)c * {D} + a) * n_nodes"
+                 f" : gt + ((size_t)c * {Dout} + (a - {D})) * n_nodes;")
+        L.append(f"    float* __restrict__ sdst = a < {D} ? sx + a * {NCB} + j : sg + (a - {D}) * {NCB} + j;")
+        L.append("    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);")
+        L.append("    if (vec && j + 4 <= cnt) {")
+        L.append("      v = *reinterpret_cast<const float4*>(src + nb + j);")
+        L.append("    } else {")
+        L.append("      if (j + 0 < cnt) v.x = src[nb + j + 0];")
+        L.append("      if (j + 1 < cnt) v.y = src[nb + j + 1];")
+        L.append("      if (j + 2 < cnt) v.z = src[nb + j + 2];")
+        L.append("      if (j + 3 < cnt) v.w = src[nb + j + 3];")
+        L.append("    }")
+        L.append("    *reinterpret_cast<float4*>(sdst) = v;")
+        L.append("  }")
     L.append("  __syncthreads();")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
     L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {nt};")
@@ -1019,16 +1051,16 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"        const int o = sb * {64 * NPL} + {NPL} * lane;")
         if NPL == 1:
             for a in sorted(need_x):
-                L.append(f"        const float x{a} = sx[{a * NCB} + o];")
+                L.append(f"        const float x{a} = sx[{a * SXS} + o];")
             for q in sorted(need_g):
-                L.append(f"        const float g{q} = sg[{q * NCB} + o];")
+                L.append(f"        const float g{q} = sg[{q * SXS} + o];")
             halves = [""]
         else:
             # adjacent nodes o, o + 1 of one operand in one 8-byte read; the terms run per node
             for a in sorted(need_x):
-                L.append(f"        const float2 x{a} = *reinterpret_cast<const float2*>(&sx[{a * NCB} + o]);")
+                L.append(f"        const float2 x{a} = *reinterpret_cast<const float2*>(&sx[{a * SXS} + o]);")
             for q in sorted(need_g):
-                L.append(f"        const float2 g{q} = *reinterpret_cast<const float2*>(&sg[{q * NCB} + o]);")
+                L.append(f"        const float2 g{q} = *reinterpret_cast<const float2*>(&sg[{q * SXS} + o]);")
             halves = [".x", ".y"]
         for h in halves:
             cur = None
@@ -1061,6 +1093,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("}")
     WPB, NBC = WV, NCB
     info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
+                coef_mulmajor=SC_COEF_MULMAJOR,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -1106,7 +1139,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}}},')
+                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}, {i["coef_mulmajor"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -36,12 +36,13 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk} (D: coupling
- * components per channel of the input, D_out: of the output; they differ when the product maps
- * the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node chunk of
- * eelg_sc_bwd_coef) */
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk, coef_mulmajor}
+ * (D: coupling components per channel of the input, D_out: of the output; they differ when the
+ * product maps the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node
+ * chunk of eelg_sc_bwd_coef; coef_mulmajor: 1 if eelg_sc_bwd_coef takes the mul-major x /
+ * grad_out rows, 0 if it takes the channel-major copies of eelg_sc_bwd_x_cm) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info7, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info8, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -138,13 +139,15 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
  * which = 0: input (coupling) layout, 1: output layout. */
 int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
                    void* stream);
-/* Coefficient gradient from channel-major x and grad_out (replaces the weight gradient
- * through the U.W contraction of gnn/mace.py:242-277):
- * partial[n_chunks, mul, nterms], n_chunks = ceil(n_nodes / chunk); chunk must be the
- * config's coef_chunk (eelg_sc_info info[6]): one workgroup keeps that many nodes of one
- * channel resident in LDS.  The caller sums over chunks (deterministic). */
-int eelg_sc_bwd_coef(int cfg, const float* xt, const float* grad_out_t, int n_nodes, int mul,
-                     int chunk, float* partial, void* stream);
+/* Coefficient gradient (replaces the weight gradient through the U.W contraction of
+ * gnn/mace.py:242-277) from x and grad_out: the mul-major rows [N, x_row] / [N, out_row] when
+ * the config's coef_mulmajor (eelg_sc_info info[7]) is 1, else their channel-major copies
+ * xt[(c*D + a)*N + n] / gt (eelg_sc_bwd_x_cm).  partial[n_chunks, mul, nterms],
+ * n_chunks = ceil(n_nodes / chunk); chunk must be the config's coef_chunk (info[6]): one
+ * workgroup keeps that many nodes of one channel resident in LDS.  The caller sums over
+ * chunks (deterministic). */
+int eelg_sc_bwd_coef(int cfg, const float* x_or_xt, const float* grad_out_or_gt, int n_nodes,
+                     int mul, int chunk, float* partial, void* stream);
 
 /* Channel-mixing linear on mul-major irreps rows (o3.Linear, gnn/blocks.py:516-521,
  * 553-559,471-476; gnn/model.py:82-86), fp32 MFMA.  A descriptor lists output

@@ -361,24 +361,31 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
     D, Do, nt, chunk = info["D"], info["Dout"], info["nterms"], info["coef_chunk"]
     assert len(plan.terms) == nt
     torch.manual_seed(n)
-    xt = torch.randn(32 * D, n, device=DEV)
-    gt = torch.randn(32 * Do, n, device=DEV)
+    # mul-major rows (e3nn layout) and their channel-major view [32, D, n]
+    x = torch.randn(n, 32 * D, device=DEV)
+    g = torch.randn(n, 32 * Do, device=DEV)
+
+    def cmajor(rows):
+        blocks = [rows[:, 32 * l * l: 32 * (l + 1) ** 2].reshape(n, 32, 2 * l + 1) for l in range(lmax + 1)]
+        return torch.cat(blocks, 2).permute(1, 2, 0).contiguous()          # [32, D, n]
+    xt, gt = cmajor(x), cmajor(g)
+    ops_x, ops_g = (x, g) if info["coef_mulmajor"] else (xt, gt)
     nch = -(-n // chunk)
     part = torch.full((nch, 32, nt), float("nan"), device=DEV)
     lib = _lib.load()
-    _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(xt), _lib.ptr(gt), n, 32, chunk, _lib.ptr(part),
+    _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(ops_x), _lib.ptr(ops_g), n, 32, chunk, _lib.ptr(part),
                                     _lib.stream(part)), "sc_bwd_coef")
     got = part.sum(0)
     # wrong chunk sizes are rejected, not silently mis-tiled
     with pytest.raises(_lib.EELGError):
-        _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(xt), _lib.ptr(gt), n, 32, chunk * 2,
+        _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(ops_x), _lib.ptr(ops_g), n, 32, chunk * 2,
                                         _lib.ptr(part), _lib.stream(part)), "sc_bwd_coef")
     A = torch.tensor([a for _, (a, b, c), q in plan.terms], device=DEV)
     B = torch.tensor([b if b >= 0 else D for _, (a, b, c), q in plan.terms], device=DEV)
     C = torch.tensor([c if c >= 0 else D for _, (a, b, c), q in plan.terms], device=DEV)
     Q = torch.tensor([q for _, (a, b, c), q in plan.terms], device=DEV)
-    X = torch.cat([xt.view(32, D, n).double(), torch.ones(32, 1, n, device=DEV, dtype=torch.float64)], 1)
-    G = gt.view(32, Do, n).double()
+    X = torch.cat([xt.double(), torch.ones(32, 1, n, device=DEV, dtype=torch.float64)], 1)
+    G = gt.double()
     want = torch.stack([(X[c, A] * X[c, B] * X[c, C] * G[c, Q]).sum(-1) for c in range(32)])
     assert torch.isfinite(got).all()
     assert rel_err(got, want) < 1e-5
