@@ -632,6 +632,16 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
 # symmetric contraction
 # ---------------------------------------------------------------------------
 def pin(vs: List[str], memory: bool = False, sgprs: Sequence[str] = ()) -> str:
+    if SC_PK == 3 and PIN_FIELDS:
+        vs = [f for v in vs for f in ((v,) if v.startswith("acc[") or v.startswith("red[") else
+                                      (f"{v}.x", f"{v}.y"))]
+    return _pin(vs, memory, sgprs)
+
+
+PIN_FIELDS = False      # set while emitting the SC_PK=3 fwd / grad-x bodies
+
+
+def _pin(vs: List[str], memory: bool = False, sgprs: Sequence[str] = ()) -> str:
     """Empty asm that 'modifies' every listed register: a hard boundary for the
     scheduler, so each term block computes in place (without it hipcc hoists
     thousands of monomials / scalar coefficient loads and spills).  ``sgprs`` are
@@ -686,6 +696,15 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     coefficients come through scalar loads), one lane = one node.  The output irreps
     (``ls``, parity (-1)^l) may differ from the coupling irreps of the input (the
     reference's product block maps the interaction irreps onto the hidden irreps)."""
+    global PIN_FIELDS
+    PIN_FIELDS = SC_PK == 3
+    try:
+        return _emit_sc(name, coupling, ls, corr)
+    finally:
+        PIN_FIELDS = False
+
+
+def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
     plan = cg.symcon_plan(coupling, ls, corr)
     irs = [ir for _, ir in Irreps(coupling)]
     out_irs = [Ir(l, (-1) ** l) for l in ls]
@@ -735,10 +754,13 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    PKN = SC_PK
+    # SC_PK: 1 = one node per lane; 2 = two nodes per lane in packed fp32 (v_pk_*); 3 = two
+    # nodes per lane in plain fp32 (a two-float struct: every coefficient scalar load and LDS
+    # coefficient fetch feeds two independent FMAs, no packed-operand constraints)
+    PKN = 2 if SC_PK in (2, 3) else 1
     NB = 64 * PKN                           # nodes per workgroup (fwd / grad-x)
-    FT = "float" if PKN == 1 else "eelg_f2"
-    ZERO = "0.0f" if PKN == 1 else "eelg_f2{0.0f, 0.0f}"
+    FT = {1: "float", 2: "eelg_f2", 3: "eelg_d2"}[SC_PK]
+    ZERO = "0.0f" if PKN == 1 else f"{FT}{{0.0f, 0.0f}}"
 
     def fma_s(c, v, acc):
         """acc + c * v, c a wave-uniform scalar coefficient"""
@@ -750,7 +772,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     def ld_pair(dst, base0, base1, col):
         if PKN == 1:
             return f"{FT} {dst} = {base0}[{col}];"
-        return f"{FT} {dst} = eelg_f2{{{base0}[{col}], {base1}[{col}]}};"
+        return f"{FT} {dst} = {FT}{{{base0}[{col}], {base1}[{col}]}};"
 
     def st_pair(val, base0, base1, col):
         if PKN == 1:
@@ -960,7 +982,6 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # of a 64-node sub-tile) with no further barrier.  The per-lane sums are reduced over the
     # 64 lanes by recursive halving (eelg_lane_reduce64), so lane t ends with term t of the
     # group.  Deterministic partials part[chunk, c, t], summed over chunks by the caller.
-    assert PKN == 1, "packed fp32 coefficient gradient is not generated"
     NCB = SC_COEF_CHUNK
     WV = SC_COEF_WAVES
     NPL = SC_COEF_NPL
@@ -1113,7 +1134,14 @@ def main(outdir: str) -> None:
              "__device__ __forceinline__ eelg_f2 eelg_fma2(eelg_f2 a, eelg_f2 b, eelg_f2 c) {"
              " return __builtin_elementwise_fma(a, b, c); }",
              "__device__ __forceinline__ eelg_f2 eelg_fma2s(float a, eelg_f2 b, eelg_f2 c) {"
-             " return __builtin_elementwise_fma(eelg_f2{a, a}, b, c); }", ""]
+             " return __builtin_elementwise_fma(eelg_f2{a, a}, b, c); }",
+             "// two nodes per lane in plain fp32 (EELG_SC_PK=3): a struct, so no packed ops form",
+             "struct eelg_d2 { float x, y; };",
+             "__device__ __forceinline__ eelg_d2 operator*(eelg_d2 a, eelg_d2 b) { return {a.x * b.x, a.y * b.y}; }",
+             "__device__ __forceinline__ eelg_d2 eelg_fma2(eelg_d2 a, eelg_d2 b, eelg_d2 c) {"
+             " return {fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }",
+             "__device__ __forceinline__ eelg_d2 eelg_fma2s(float a, eelg_d2 b, eelg_d2 c) {"
+             " return {fmaf(a, b.x, c.x), fmaf(a, b.y, c.y)}; }", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     tp_table, sc_table = [], []

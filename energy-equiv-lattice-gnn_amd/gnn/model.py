@@ -123,6 +123,17 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         return self.positive_layer(self.cart_to_Mandel(stiff))
 
 
+def _embed(lin: torch.nn.Linear, attrs: torch.Tensor) -> torch.Tensor:
+    """``Linear(1 -> 32)`` of the node attributes (``gnn/model.py:122,142``).  With one input
+    feature it is an outer product plus bias: one broadcast multiply-add instead of a K = 1
+    library GEMM (0.19 ms per step on MI355X for [32768 x 1] x [1 x 32], r02q), and its weight
+    gradient is a column sum.  Same values (a single product per output plus the bias)."""
+    if lin.in_features != 1:
+        return lin(attrs)
+    return torch.addcmul(lin.bias, attrs, lin.weight[:, 0]) if lin.bias is not None \
+        else attrs * lin.weight[:, 0]
+
+
 class EnergyEquivGNN(torch.nn.Module):
     def __init__(self, params: Namespace, *args: Any, **kwargs: Any) -> None:
         super().__init__(*args, **kwargs)
@@ -169,7 +180,7 @@ class EnergyEquivGNN(torch.nn.Module):
 
     def _forward(self, batch) -> Dict[str, torch.Tensor]:
         csr = self.edge_graph(batch)
-        node_ft = self.node_ft_embedding(batch.node_attrs)
+        node_ft = _embed(self.node_ft_embedding, batch.node_attrs)
         shifts = batch.shifts[csr.perm]
         radius = batch.edge_attr[csr.perm].reshape(-1)
         edge_sh, edge_feats = ops.edge_embed(batch.positions, csr, shifts, radius, self.lmax,
