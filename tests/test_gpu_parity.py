@@ -326,14 +326,15 @@ def test_stream_overlap_matches_in_line_bitwise():
     from gnn.train import stiffness_loss
     b, bd, csr, rmax = _setup()
     p = params(4, max_edge_radius=rmax)
-    torch.manual_seed(0)
-    m = EnergyEquivGNN(p).to(DEV)
     saved = ops.OVERLAP
     outs = []
     try:
         for flag in (False, True):
             ops.OVERLAP = flag
-            m.zero_grad(set_to_none=True)
+            # one model per mode (same seed): a parameter's gradient accumulator belongs to the
+            # stream of its first backward, and production never switches modes mid-run
+            torch.manual_seed(0)
+            m = EnergyEquivGNN(p).to(DEV)
             c = m(bd)["stiffness"]
             stiffness_loss(c, bd.stiffness).backward()
             torch.cuda.synchronize()
