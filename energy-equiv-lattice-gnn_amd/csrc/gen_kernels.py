@@ -49,6 +49,10 @@ TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # 0.86): twice the VGPRs and LDS per workgroup halve the occupancy, the SGPR coefficient
 # operands need aligned pairs (s_mov per term), and dependent v_pk ops carry a wait state
 SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+# symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
+# computed, forward / grad-x (r02: grad-x 0.56 -> 0.51 ms at 3; the forward spills SGPRs at 2+)
+SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
+SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "3"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, sub-tile unroll
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
 SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
@@ -859,12 +863,14 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
         L.append(f"  {FT} o{q} = {ZERO};")
     blocks = sc_blocks(plan)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    for t in blocks[0]["terms"]:
-        L.append(f"  float c{t} = cf[{t}];")
-    for bi, blk in enumerate(blocks):
-        nxt = blocks[bi + 1]["terms"] if bi + 1 < len(blocks) else []
-        for t in nxt:
+    for b0 in blocks[:SC_PFD_FWD]:
+        for t in b0["terms"]:
             L.append(f"  float c{t} = cf[{t}];")
+    for bi, blk in enumerate(blocks):
+        # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
+        for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
+            L.append(f"  float c{t} = cf[{t}];")
+        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
@@ -921,12 +927,14 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     for q in range(Dout):
         L.append("  " + ld_pair(f"g{q}", "xr", "xr1", lq(lout, q, 'cl')))
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
-    for t in blocks[0]["terms"]:
-        L.append(f"  float c{t} = cf[{t}];")
-    for bi, blk in enumerate(blocks):
-        nxt = blocks[bi + 1]["terms"] if bi + 1 < len(blocks) else []
-        for t in nxt:
+    for b0 in blocks[:SC_PFD_BWD]:
+        for t in b0["terms"]:
             L.append(f"  float c{t} = cf[{t}];")
+    for bi, blk in enumerate(blocks):
+        # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
+        for t in (blocks[bi + SC_PFD_BWD]["terms"] if bi + SC_PFD_BWD < len(blocks) else []):
+            L.append(f"  float c{t} = cf[{t}];")
+        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_BWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:

@@ -384,6 +384,26 @@ class _nullctx:
 # ---------------------------------------------------------------------------
 # radial MLP (conv_tp_weights, gnn/blocks.py:537-549)
 # ---------------------------------------------------------------------------
+def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
+    """g^T @ x over a long row dimension as a split-K batched GEMM + fixed-order sum (the CGC
+    models' weight gradients, gnn/cgc.py; library GEMMs pick no split-K for
+    [64 x 131072] @ [131072 x 64] and run on a few CUs)."""
+    e = g.shape[0]
+    c = e // chunk
+    acc = torch.promote_types(g.dtype, torch.float32)     # bf16 operands: fp32 sums
+    out = None
+    if c > 1:
+        m = c * chunk
+        out = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2),
+                        x[:m].view(c, chunk, -1)).sum(0, dtype=acc)
+        g, x = g[m:], x[m:]
+    if g.shape[0]:
+        rest = (g.t() @ x).to(acc)
+        out = rest if out is None else out + rest
+    return out if out is not None else torch.zeros(g.shape[1], x.shape[1], device=g.device,
+                                                   dtype=acc)
+
+
 def _radial_desc(params, n_feat: int):
     n_hidden = (len(params) - 1) // 2
     hidden = params[0].shape[0]

@@ -218,6 +218,13 @@ def test_radial_mlp_is_hip_only_and_checks_shapes():
     TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=32, MLP_layers=4)
 
 
+def test_wgrad_split_k_matches_matmul():
+    from gnn.ops import _wgrad
+    g = torch.randn(1300, 8, dtype=torch.float64)
+    x = torch.randn(1300, 5, dtype=torch.float64)
+    assert torch.allclose(_wgrad(g, x, chunk=256), g.t() @ x, atol=1e-10)
+
+
 def test_lmax3_with_l4_hidden_irreps_raises_like_the_reference():
     """The reference cannot build a product block whose outputs exceed the SH lmax
     (gnn/mace.py:466-476); the product says so instead of failing inside numpy."""
