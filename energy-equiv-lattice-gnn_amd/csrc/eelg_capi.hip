@@ -184,6 +184,34 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(
   if (ok && sub == 0) out[(size_t)r * ldo_r + (size_t)c * ldo_c] = acc;
 }
 
+// Column sums of a [rows, width] row-major block: out[w] = sum_r src[r, w], rows added in order
+// (deterministic).  The per-slice / per-chunk partials of the weight-gradient kernels are summed
+// with it: a thread owns 4 columns (float4 when aligned) and streams down the rows, so every
+// wave reads contiguous 1 KB row pieces and the launch has width / 1024 workgroups.
+template <bool VEC4>
+__global__ __launch_bounds__(256) void sum_rows_kernel(const float* __restrict__ src, int rows,
+                                                       int width, float* __restrict__ out) {
+  const int c4 = blockIdx.x * 256 + threadIdx.x;
+  if (VEC4) {
+    if (4 * c4 >= width) return;
+    const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src) + c4;
+    const int w4 = width >> 2;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int r = 0; r < rows; ++r) {
+      const float4 v = s4[(size_t)r * w4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[c4] = acc;
+  } else {
+    for (int c = 4 * c4; c < min(width, 4 * c4 + 4); ++c) {
+      float acc = 0.f;
+      for (int r = 0; r < rows; ++r) acc += src[(size_t)r * width + c];
+      out[c] = acc;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -348,6 +376,18 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
   return check_launch("segment_sum_split");
 }
 
+int eelg_sum_rows(const float* src, int rows, int width, float* out, void* stream) {
+  if (rows < 0 || width < 0) return fail(-2, "sum_rows: negative size");
+  if (width == 0) return 0;
+  const dim3 grid((width + 1023) / 1024);
+  const bool vec = (width % 4 == 0) && ((uintptr_t)src % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL(sum_rows_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, src, rows, width, out);
+  else
+    hipLaunchKernelGGL(sum_rows_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src, rows, width, out);
+  return check_launch("sum_rows");
+}
+
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
                  void* stream) {
@@ -438,8 +478,9 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
   return check_launch("sc_bwd_coef");
 }
 
-int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
-                    float* y, int y_row, const eelg_lin_desc* desc, void* stream) {
+int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* bias,
+                        const float* res, int n_nodes, float* y, int y_row,
+                        const eelg_lin_desc* desc, void* stream) {
   if (!desc || desc->n_slots <= 0 || desc->n_slots > EELG_LIN_MAXSLOT)
     return fail(-2, "linear_fwd: bad descriptor");
   for (int s = 0; s < desc->n_slots; ++s) {
@@ -451,7 +492,7 @@ int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias
     if (sl.bias_off >= 0 && sl.d != 1) return fail(-2, "linear_fwd: bias on a non-scalar slot");
   }
   if (n_nodes <= 0) return 0;
-  if (lin_fwd_fast_ok(x, x_row, y, y_row, desc)) {
+  if (lin_fwd_fast_ok(x, x_row, y, y_row, desc) && !(res && (reinterpret_cast<uintptr_t>(res) & 15))) {
     // groups of 32/d whole nodes; the d = 9 slots have the most (ceil(n / 3))
     int max_groups = 0;
     for (int s = 0; s < desc->n_slots; ++s) {
@@ -462,13 +503,18 @@ int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias
     const int gblocks = (max_groups + LINF_WAVES * LINF_GPW - 1) / (LINF_WAVES * LINF_GPW);
     dim3 grid(((gblocks + 7) / 8) * 8 * desc->max_jt, desc->n_slots, 1);
     hipLaunchKernelGGL(lin_fwd_fast_kernel, grid, dim3(64 * LINF_WAVES), 0, (hipStream_t)stream, x,
-                       x_row, w, bias, n_nodes, y, y_row, *desc);
+                       x_row, w, bias, n_nodes, y, y_row, *desc, res);
     return check_launch("linear_fwd");
   }
   dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, 1);  // column tiles loop in-kernel
   hipLaunchKernelGGL(lin_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, w, bias,
-                     n_nodes, y, y_row, *desc);
+                     n_nodes, y, y_row, *desc, res);
   return check_launch("linear_fwd");
+}
+
+int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
+                    float* y, int y_row, const eelg_lin_desc* desc, void* stream) {
+  return eelg_linear_fwd_res(x, x_row, w, bias, nullptr, n_nodes, y, y_row, desc, stream);
 }
 
 int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,

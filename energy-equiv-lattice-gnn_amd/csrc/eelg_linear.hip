@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ bias, int n_nodes,
                                                       float* __restrict__ y, int y_row,
-                                                      eelg_lin_desc desc) {
+                                                      eelg_lin_desc desc,
+                                                      const float* __restrict__ res) {
   __shared__ float As[LIN_ROWS * LIN_ST];
   __shared__ float Bs[LIN_KC * LIN_ST];
   __shared__ float Os[LIN_ROWS * LIN_ST];
@@ -206,8 +207,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
     const int jw = min(32, sl.n_out - jt * 32);
     const int olen = jw * d;  // floats per node in this column tile
     float* __restrict__ yb = y + (size_t)n_lo * y_row + sl.y_off + (size_t)jt * 32 * d;
+    // optional residual (same layout as y) added in the epilogue
+    const float* __restrict__ rb = res ? res + (size_t)n_lo * y_row + sl.y_off + (size_t)jt * 32 * d : nullptr;
     const bool vst = (y_row & 3) == 0 && (olen & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
-                     ((sl.y_off + jt * 32 * d) & 3) == 0;
+                     ((sl.y_off + jt * 32 * d) & 3) == 0 && (reinterpret_cast<uintptr_t>(res) & 15) == 0;
     if (vst) {
       // float4 per-node runs; nodes cut by the workgroup's row range go element-wise
       Walk3 ow;
@@ -223,12 +226,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
             v[t] = Os[(nrow0 + m) * LIN_ST + jj];
             if (++m == d) { m = 0; ++jj; }
           }
+          if (rb) {
+            const float4 r4 = *reinterpret_cast<const float4*>(rb + (dst - yb));
+            v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+          }
           *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int row = nrow0 + m;
-            if (row >= 0 && row < LIN_ROWS) dst[t] = Os[row * LIN_ST + jj];
+            if (row >= 0 && row < LIN_ROWS) dst[t] = Os[row * LIN_ST + jj] + (rb ? rb[(dst - yb) + t] : 0.0f);
             if (++m == d) { m = 0; ++jj; }
           }
         }
@@ -239,7 +246,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
       ow.init(tid, 256, jw, d);
       for (int f = tid; f < span * olen; f += 256) {
         const int row = (n_lo + ow.a) * d + ow.m - r0;
-        if (row >= 0 && row < LIN_ROWS) yb[(size_t)ow.a * y_row + ow.b * d + ow.m] = Os[row * LIN_ST + ow.b];
+        if (row >= 0 && row < LIN_ROWS) {
+          const size_t o = (size_t)ow.a * y_row + ow.b * d + ow.m;
+          yb[o] = Os[row * LIN_ST + ow.b] + (rb ? rb[o] : 0.0f);
+        }
         ow.next(jw, d);
       }
     }
@@ -513,7 +523,8 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
                                              const float* __restrict__ bias, int n_nodes,
                                              float* __restrict__ y, int y_row,
                                              const eelg_lin_slot& sl, int gb, int jt,
-                                             const float* __restrict__ ws, float* __restrict__ xw) {
+                                             const float* __restrict__ ws, float* __restrict__ xw,
+                                             const float* __restrict__ res) {
   using G = LinfGeom<D>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
   const int n_groups = (n_nodes + G::NB - 1) / G::NB;
@@ -594,9 +605,15 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       for (int qq = 0; qq < G::NQ; ++qq) {
         const int f = lane + 64 * qq;
         const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-        if (f < G::NB * G::RUN4 && n0 + a < n_nodes)
-          *reinterpret_cast<float4*>(yb + (size_t)(n0 + a) * y_row + 4 * w4) =
-              *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
+        if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
+          const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
+          float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
+          if (res) {   // residual (same layout as y) added in the epilogue
+            const float4 r4 = *reinterpret_cast<const float4*>(res + sl.y_off + (size_t)jt * 32 * D + o);
+            v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
+          }
+          *reinterpret_cast<float4*>(yb + o) = v;
+        }
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -618,7 +635,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
 __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
     const float* __restrict__ x, int x_row, const float* __restrict__ w,
     const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
-    eelg_lin_desc desc) {
+    eelg_lin_desc desc, const float* __restrict__ res) {
   __shared__ float ws[LINF_KMAX * 32];
   __shared__ float4 xw4[LINF_WAVES * LINF_XW / 4];
   // the last slots (highest l, the most rows) are dispatched first: a shorter tail
@@ -646,11 +663,11 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   __syncthreads();
   float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
   switch (d) {
-    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
-    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
-    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
-    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
-    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw); break;
+    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
+    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
+    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
+    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
+    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
   }
 }
 

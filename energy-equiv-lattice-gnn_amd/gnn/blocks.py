@@ -144,8 +144,10 @@ class EquivariantProductBlock(torch.nn.Module):
         self.symmetric_contractions = SymmetricContraction(node_feats_irreps, sc_out, correlation)
         self.linear = Linear(sc_out, target_irreps)
 
-    def forward(self, node_feats, sc):
-        x = self.linear(self.symmetric_contractions(node_feats))
+    def forward(self, node_feats, sc, residual: Optional[torch.Tensor] = None):
+        """``residual``: the model's layer residual (``gnn/model.py:95``), added in the linear's
+        epilogue instead of by a separate pass."""
+        x = self.linear(self.symmetric_contractions(node_feats), residual=residual)
         return x + sc if self.use_sc else x
 
 
@@ -243,9 +245,11 @@ class MACELayer(torch.nn.Module):
                                                product_correlation, use_sc=False)
 
     def forward(self, node_ft, edge_index: EdgeIndex, edge_sh, edge_scalars,
-                tp_weights: Optional[torch.Tensor] = None):
+                tp_weights: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None):
+        """``residual`` (default none): returns ``residual + layer(node_ft)`` with the add fused
+        into the product block's linear (``GNN_Head`` passes ``h`` for ``h + layer_i(h)``)."""
         csr, edge_sh, edge_scalars = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_scalars)
         if tp_weights is not None and not isinstance(edge_index, ops.EdgeCSR):
             tp_weights = tp_weights[csr.perm]
         node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr, tp_weights=tp_weights)
-        return self.product(node_ft, sc)
+        return self.product(node_ft, sc, residual=residual)

@@ -106,17 +106,19 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         csr, edge_sh, edge_feats = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_feats)
         ws, evs = self._radial_weights_ahead(edge_feats)
 
-        def run(i, h):
+        def run(i, h, residual=None):
             if evs[i] is not None:
                 torch.cuda.current_stream(h.device).wait_event(evs[i])
-            return self.layers[i](h, csr, edge_sh, edge_feats, tp_weights=ws[i])
+            return self.layers[i](h, csr, edge_sh, edge_feats, tp_weights=ws[i], residual=residual)
 
         node_ft = run(0, node_ft)
         if RADIAL_AHEAD_OF_LAYER1 and evs[-1] is not None:
             # the later layers' interaction kernels run without the MLP GEMMs beside them
             torch.cuda.current_stream(node_ft.device).wait_event(evs[-1])
         for i in range(1, self.num_interactions):
-            node_ft = node_ft + run(i, node_ft)
+            # node_ft + layer_i(node_ft) (gnn/model.py:95), the add fused into the layer's
+            # last linear
+            node_ft = run(i, node_ft, residual=node_ft)
         out = self.nonlin_readout(node_ft)
         graph_ft = ops.graph_pool(out, batch_idx, num_graphs, self.global_reduction)
         stiff = self.sph_to_cart(self.linear(graph_ft))

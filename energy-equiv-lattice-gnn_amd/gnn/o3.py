@@ -49,10 +49,10 @@ class _OnStream(torch.autograd.Function):
 
 class _IrrepsLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, lin: "Linear", side=None):
+    def forward(ctx, x, weight, bias, lin: "Linear", side=None, residual=None):
         ctx.save_for_backward(x, weight)
         ctx.lin, ctx.side = lin, side
-        return lin._fwd(x, weight, bias)
+        return lin._fwd(x, weight, bias, residual)
 
     @staticmethod
     def backward(ctx, gy):
@@ -61,10 +61,11 @@ class _IrrepsLinearFn(torch.autograd.Function):
         gy = gy.contiguous()
         gx = lin._bwd_x(gy, weight) if ctx.needs_input_grad[0] else None
         want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        gres = gy if ctx.needs_input_grad[5] else None      # y = linear(x) + residual
         if side is None or not (want_w or want_b):
             gw = lin._bwd_w(x, gy) if want_w else None
             gb = lin._bwd_bias(gy) if want_b else None
-            return gx, gw, gb, None, None
+            return gx, gw, gb, None, None, gres
         # weight / bias gradients on the side stream the parameters' views were made on:
         # their consumers (the views' backward, the accumulation) run there as well, and
         # the main stream carries on with grad-x
@@ -74,7 +75,7 @@ class _IrrepsLinearFn(torch.autograd.Function):
         with torch.cuda.stream(side):
             gw = lin._bwd_w(x, gy) if want_w else None
             gb = lin._bwd_bias(gy) if want_b else None
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, gres
 
 
 class Linear(torch.nn.Module):
@@ -172,14 +173,19 @@ class Linear(torch.nn.Module):
                              for i, o in self.instructions) or 1
 
     # -- launches ---------------------------------------------------------------
-    def _fwd(self, x, weight, bias):
+    def _fwd(self, x, weight, bias, residual=None):
         from . import _lib
         n = x.shape[0]
         y = torch.empty(n, self.irreps_out.dim, device=x.device, dtype=torch.float32)
         self._fwd_desc.max_rows = n * self._fwd_maxd
-        _lib.check(_lib.load().eelg_linear_fwd(
-            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(weight), _lib.ptr(bias), n, _lib.ptr(y),
-            self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream(y)), "linear_fwd")
+        if residual is not None and (residual.shape != y.shape or residual.dtype != torch.float32
+                                     or not residual.is_contiguous()):
+            raise ValueError(f"residual {tuple(residual.shape)} {residual.dtype}: expected a "
+                             f"contiguous float32 {tuple(y.shape)}")
+        _lib.check(_lib.load().eelg_linear_fwd_res(
+            _lib.ptr(x), self.irreps_in.dim, _lib.ptr(weight), _lib.ptr(bias), _lib.ptr(residual), n,
+            _lib.ptr(y), self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream(y)),
+            "linear_fwd")
         return y
 
     def _bwd_x(self, gy, weight):
@@ -207,14 +213,17 @@ class Linear(torch.nn.Module):
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, nps,
             _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream(part)),
             "linear_bwd_w")
-        return part.sum(0)
+        from .ops import sum_rows
+        return sum_rows(part)
 
     def _bwd_bias(self, gy):
         parts = [gy[:, self._out_off[o]: self._out_off[o] + self.irreps_out[o].mul].sum(0)
                  for o in self.bias_slots]
         return torch.cat(parts)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: torch.Tensor = None) -> torch.Tensor:
+        """``o3.Linear``; with ``residual`` returns ``linear(x) + residual`` with the add in the
+        kernel epilogue (the layer residual of ``gnn/model.py:92-96``)."""
         from .ops import _f32, _require_device
         _require_device(x)
         if x.shape[-1] != self.irreps_in.dim:
@@ -228,7 +237,10 @@ class Linear(torch.nn.Module):
                 weight = _OnStream.apply(weight, side)
                 if bias is not None:
                     bias = _OnStream.apply(bias, side)
-        return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side)
+        if residual is not None:
+            _require_device(residual)
+            residual = _f32(residual)
+        return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side, residual)
 
 
 class Gate(torch.nn.Module):

@@ -99,6 +99,12 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
                            const float* row_scale, float scale, int n_rows, int width, int n_split,
                            float* work, float* out, void* stream);
 
+/* Column sums out[w] = sum_r src[r, w] of a [rows, width] row-major block, rows in order
+ * (deterministic): the caller-side sum of the per-slice / per-chunk partials that the
+ * weight-gradient kernels below write (eelg_linear_bwd_w, eelg_sc_bwd_coef, eelg_radial_bwd),
+ * i.e. the reduction autograd performs for the reference's weight gradients. */
+int eelg_sum_rows(const float* src, int rows, int width, float* out, void* stream);
+
 /* Crystal-graph edge convolution (CGC/mCGC benchmark models): replaces
  *   c = cat([x[sender], x[receiver], edge_ft]); msg = softplus(fc_values(c)) * sigmoid(fc_multip(c));
  *   scatter(msg, receiver, reduce)          (scripts/benchmark_models/cgc_modified.py:20-25,
@@ -161,6 +167,12 @@ typedef struct { int y_off, n_out, d, bias_off, n_src; eelg_lin_src src[EELG_LIN
 typedef struct { int n_slots, max_jt, max_rows, pad; eelg_lin_slot slot[EELG_LIN_MAXSLOT]; } eelg_lin_desc;
 int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,
                     float* y, int y_row, const eelg_lin_desc* desc, void* stream);
+/* eelg_linear_fwd plus a residual res (y's layout, may be NULL) added in the epilogue:
+ * y = linear(x) + res, the layer residual h + layer_i(h) of gnn/model.py:92-96 with the
+ * product block's o3.Linear (gnn/blocks.py:486) producing layer_i(h). */
+int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* bias,
+                        const float* res, int n_nodes, float* y, int y_row,
+                        const eelg_lin_desc* desc, void* stream);
 
 /* grad of the weights: partial[p, w_off + u*n_out + j] over node slices p of
  * nodes_per_slice nodes (sum over p on the caller side; deterministic).

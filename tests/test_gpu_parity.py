@@ -390,3 +390,36 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
     want = torch.stack([(X[c, A] * X[c, B] * X[c, C] * G[c, Q]).sum(-1) for c in range(32)])
     assert torch.isfinite(got).all()
     assert rel_err(got, want) < 1e-5
+
+
+@pytest.mark.parametrize("rows,width", [(49, 43040), (64, 240608), (1, 7), (3, 5), (0, 8), (186, 86016)])
+def test_sum_rows_matches_torch(rows, width):
+    """eelg_sum_rows (the weight-gradient partial sums) against torch.sum in fp64."""
+    from gnn import ops
+    torch.manual_seed(rows + width)
+    part = torch.randn(rows, width, device=DEV)
+    got = ops.sum_rows(part)
+    want = part.double().sum(0)
+    assert got.shape == (width,)
+    assert float((got.double() - want).abs().max()) <= 1e-5 * max(1.0, float(want.abs().max()))
+
+
+@pytest.mark.parametrize("irreps", ["32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+16x0e+32x1o"])
+def test_linear_residual_epilogue(irreps):
+    """Linear(x, residual) == Linear(x) + residual in value and in every gradient (the fused
+    layer residual), on the fast path (first irreps) and the general path (second)."""
+    from gnn.o3 import Linear
+    torch.manual_seed(3)
+    lin = Linear(irreps, irreps).to(DEV)
+    n = 301
+    x = torch.randn(n, lin.irreps_in.dim, device=DEV, requires_grad=True)
+    r = torch.randn(n, lin.irreps_out.dim, device=DEV, requires_grad=True)
+    g = torch.randn(n, lin.irreps_out.dim, device=DEV)
+    y1 = lin(x, residual=r)
+    (y1 * g).sum().backward()
+    gx1, gr1, gw1 = x.grad.clone(), r.grad.clone(), lin.weight.grad.clone()
+    x.grad = r.grad = lin.weight.grad = None
+    y2 = lin(x) + r
+    (y2 * g).sum().backward()
+    assert torch.allclose(y1, y2, atol=1e-6, rtol=1e-6)
+    assert torch.equal(gx1, x.grad) and torch.equal(gr1, r.grad) and torch.equal(gw1, lin.weight.grad)
