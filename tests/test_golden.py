@@ -41,6 +41,7 @@ def set_params(model, g):
 
 def rel(a, b):
     a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double()
+    a, b = a.detach(), b.detach()
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
 
 
