@@ -15,7 +15,8 @@
 // out-of-range offset (past the end, or RAD_OOB for a masked lane) into a zero load / a
 // dropped store.
 //
-// Forward (radial_fwd): one wave owns 32 edges end to end.  Hidden activations stay in a
+// Forward (radial_fwd): one wave owns 32 edges end to end; the output layer's W_o tiles are
+// shared by the workgroup's 4 waves through LDS.  Hidden activations stay in a
 // wave-private LDS tile; only the pre-activations z_n (the backward's operand,
 // [NH, E, H]) and w reach HBM.
 // Backward (deterministic: per-wave / per-split partials, summed by the caller in a fixed
@@ -81,9 +82,12 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
                                                          void* __restrict__ out) {
   constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4;
   __shared__ float hb[4 * 32 * HS];
+  __shared__ float bt[2][H * 32];   // W_o^T column tile [k][j], double-buffered, shared by 4 waves
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
   const int e0 = (blockIdx.x * 4 + wave) * 32;
-  if (e0 >= n_edges) return;  // wave-uniform; the kernel has no workgroup barrier
+  // waves past the last edge skip the hidden layers but join the output layer's barriers
+  // (their stores fall outside the buffer range)
+  const bool active = e0 < n_edges;
   float* __restrict__ hw = hb + wave * 32 * HS;
   const int F = d.n_feat, W = d.n_out;
   const uint32_t E = (uint32_t)n_edges;
@@ -100,6 +104,7 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
   }
 #pragma unroll
   for (int n = 0; n < NH; ++n) {
+    if (!active) break;   // wave-uniform
     const float* __restrict__ wn = d.w[n];
     const float* __restrict__ bn = d.b[n];
     const int din = n == 0 ? F : H;
@@ -135,23 +140,37 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
         hw[row * HS + col] = rad_silu(z);
       }
   }
-  // output layer: w[e0 + row, ct*32 + i], B[k][j] = W_o[j][k] = woT[k][j] (coalesced rows)
+  // output layer: w[e0 + row, ct*32 + i], B[k][j] = W_o[j][k] = woT[k][j].  Each 32-column
+  // tile of W_o^T (H x 32 floats) is loaded once per workgroup (coalesced rows, the next tile in
+  // registers while the current one computes) and read by the 4 waves from LDS: one L2 read
+  // of W_o per 128 edges instead of per 32.
 #pragma unroll
   for (int st = 0; st < KH; ++st) a[st] = hw[i * HS + hf * KH + st];
   const int nct = (W + 31) >> 5;
-  float bc[KH], bnx[KH];
+  constexpr int BPT = H * 32 / 256;   // tile floats per thread
+  float rb[BPT];
+  auto load_b = [&](int ct) {
 #pragma unroll
-  for (int st = 0; st < KH; ++st) bc[st] = rad_ld(woT, (size_t)(hf * KH + st) * W + i, i < W);
+    for (int q = 0; q < BPT; ++q) {
+      const int e = threadIdx.x + 256 * q, k = e >> 5, col = ct * 32 + (e & 31);
+      rb[q] = rad_ld(woT, (size_t)k * W + col, col < W);
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) bt[buf][threadIdx.x + 256 * q] = rb[q];
+  };
+  load_b(0);
+  store_b(0);
+  __syncthreads();
   for (int ct = 0; ct < nct; ++ct) {
-    const int coln = (ct + 1) * 32 + i;
-#pragma unroll
-    for (int st = 0; st < KH; ++st)
-      bnx[st] = rad_ld(woT, (size_t)(hf * KH + st) * W + coln, coln < W);
+    if (ct + 1 < nct) load_b(ct + 1);
+    const float* __restrict__ bb = bt[ct & 1] + hf * KH * 32 + i;
     rad_f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 #pragma unroll
-    for (int st = 0; st < KH; ++st) acc = RAD_MFMA(a[st], bc[st], acc);
+    for (int st = 0; st < KH; ++st) acc = RAD_MFMA(a[st], bb[st * 32], acc);
     const int col = ct * 32 + i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -161,8 +180,8 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
       else
         rad_bst(ro, off, acc[r]);
     }
-#pragma unroll
-    for (int st = 0; st < KH; ++st) bc[st] = bnx[st];
+    if (ct + 1 < nct) store_b((ct + 1) & 1);
+    __syncthreads();
   }
 }
 
