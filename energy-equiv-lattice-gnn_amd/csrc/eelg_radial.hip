@@ -74,26 +74,32 @@ __device__ __forceinline__ int rad_row(int r, int hf) { return (r & 3) + 8 * (r 
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
+#ifndef RAD_FWD_RT
+#define RAD_FWD_RT 1   // 32-edge row tiles per wave (each W_o fragment read from LDS feeds RT MFMAs)
+#endif
 template <int H, int NH, bool BF>
 __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict__ feats,
                                                          int n_edges, eelg_radial_desc d,
                                                          const float* __restrict__ woT,
                                                          float* __restrict__ zsave,
                                                          void* __restrict__ out) {
-  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4;
-  __shared__ float hb[4 * 32 * HS];
+  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4, RT = RAD_FWD_RT;
+  __shared__ float hb[4 * RT * 32 * HS];
   __shared__ float bt[2][H * 32];   // W_o^T column tile [k][j], double-buffered, shared by 4 waves
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
-  const int e0 = (blockIdx.x * 4 + wave) * 32;
-  // waves past the last edge skip the hidden layers but join the output layer's barriers
-  // (their stores fall outside the buffer range)
-  const bool active = e0 < n_edges;
-  float* __restrict__ hw = hb + wave * 32 * HS;
+  const int e00 = (blockIdx.x * 4 + wave) * 32 * RT;
   const int F = d.n_feat, W = d.n_out;
   const uint32_t E = (uint32_t)n_edges;
   const rad_rsrc_t rz = rad_rsrc(zsave, (uint32_t)NH * E * H * 4u);
   const rad_rsrc_t ro = rad_rsrc(out, E * (uint32_t)W * ES);
   const int KF = (F + 1) >> 1;  // layer 0: K = F (<= 32) split over the two lane halves
+#pragma unroll 1
+  for (int rt = 0; rt < RT; ++rt) {
+  const int e0 = e00 + 32 * rt;
+  // waves / tiles past the last edge skip the hidden layers but join the output layer's
+  // barriers (their stores fall outside the buffer range)
+  const bool active = e0 < n_edges;
+  float* __restrict__ hw = hb + (wave * RT + rt) * 32 * HS;
   const bool rok = e0 + i < n_edges;
 
   float a[KH];
@@ -140,12 +146,16 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
         hw[row * HS + col] = rad_silu(z);
       }
   }
+  }
   // output layer: w[e0 + row, ct*32 + i], B[k][j] = W_o[j][k] = woT[k][j].  Each 32-column
   // tile of W_o^T (H x 32 floats) is loaded once per workgroup (coalesced rows, the next tile in
   // registers while the current one computes) and read by the 4 waves from LDS: one L2 read
   // of W_o per 128 edges instead of per 32.
+  float ar[RT][KH];
 #pragma unroll
-  for (int st = 0; st < KH; ++st) a[st] = hw[i * HS + hf * KH + st];
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int st = 0; st < KH; ++st) ar[rt][st] = hb[(wave * RT + rt) * 32 * HS + i * HS + hf * KH + st];
   const int nct = (W + 31) >> 5;
   constexpr int BPT = H * 32 / 256;   // tile floats per thread
   float rb[BPT];
@@ -166,20 +176,29 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
   for (int ct = 0; ct < nct; ++ct) {
     if (ct + 1 < nct) load_b(ct + 1);
     const float* __restrict__ bb = bt[ct & 1] + hf * KH * 32 + i;
-    rad_f32x16 acc;
+    rad_f32x16 acc[RT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int st = 0; st < KH; ++st) acc = RAD_MFMA(a[st], bb[st * 32], acc);
+      for (int r = 0; r < 16; ++r) acc[rt][r] = 0.0f;
+#pragma unroll
+    for (int st = 0; st < KH; ++st) {
+      const float bv = bb[st * 32];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = RAD_MFMA(ar[rt][st], bv, acc[rt]);
+    }
     const int col = ct * 32 + i;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t off = rad_off(((uint32_t)(e0 + rad_row(r, hf)) * W + col) * ES, col < W);
-      if (BF)
-        rad_bst16(ro, off, eelg_f2bf(acc[r]));
-      else
-        rad_bst(ro, off, acc[r]);
-    }
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t off =
+            rad_off(((uint32_t)(e00 + 32 * rt + rad_row(r, hf)) * W + col) * ES, col < W);
+        if (BF)
+          rad_bst16(ro, off, eelg_f2bf(acc[rt][r]));
+        else
+          rad_bst(ro, off, acc[rt][r]);
+      }
     if (ct + 1 < nct) store_b((ct + 1) & 1);
     __syncthreads();
   }
@@ -571,7 +590,7 @@ int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, 
   if (n_edges == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool bf = out_bf16 != 0;
-  const dim3 grid((n_edges + 127) / 128);
+  const dim3 grid((n_edges + 128 * RAD_FWD_RT - 1) / (128 * RAD_FWD_RT));
   RAD_LAUNCH3(radial_fwd_kernel, grid, feats, n_edges, *d, wo_t, zsave, out);
   return eelg_check_launch("radial_fwd");
 }
