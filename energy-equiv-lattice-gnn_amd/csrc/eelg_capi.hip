@@ -184,34 +184,6 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(
   if (ok && sub == 0) out[(size_t)r * ldo_r + (size_t)c * ldo_c] = acc;
 }
 
-// Column sums of a [rows, width] row-major block: out[w] = sum_r src[r, w], rows added in order
-// (deterministic).  The per-slice / per-chunk partials of the weight-gradient kernels are summed
-// with it: a thread owns 4 columns (float4 when aligned) and streams down the rows, so every
-// wave reads contiguous 1 KB row pieces and the launch has width / 1024 workgroups.
-template <bool VEC4>
-__global__ __launch_bounds__(256) void sum_rows_kernel(const float* __restrict__ src, int rows,
-                                                       int width, float* __restrict__ out) {
-  const int c4 = blockIdx.x * 256 + threadIdx.x;
-  if (VEC4) {
-    if (4 * c4 >= width) return;
-    const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src) + c4;
-    const int w4 = width >> 2;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-    for (int r = 0; r < rows; ++r) {
-      const float4 v = s4[(size_t)r * w4];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-    reinterpret_cast<float4*>(out)[c4] = acc;
-  } else {
-    for (int c = 4 * c4; c < min(width, 4 * c4 + 4); ++c) {
-      float acc = 0.f;
-      for (int r = 0; r < rows; ++r) acc += src[(size_t)r * width + c];
-      out[c] = acc;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -374,18 +346,6 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
   hipLaunchKernelGGL(segment_combine_kernel, dim3((n_rows * width + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, work, row_scale, scale, n_rows, width, n_split, out);
   return check_launch("segment_sum_split");
-}
-
-int eelg_sum_rows(const float* src, int rows, int width, float* out, void* stream) {
-  if (rows < 0 || width < 0) return fail(-2, "sum_rows: negative size");
-  if (width == 0) return 0;
-  const dim3 grid((width + 1023) / 1024);
-  const bool vec = (width % 4 == 0) && ((uintptr_t)src % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL(sum_rows_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, src, rows, width, out);
-  else
-    hipLaunchKernelGGL(sum_rows_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src, rows, width, out);
-  return check_launch("sum_rows");
 }
 
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,

@@ -47,7 +47,6 @@ _SIGS = {
     "eelg_linear_fwd_res": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_radial_plan": ([_I, _I, _P, _P], _I),
-    "eelg_sum_rows": ([_P, _I, _I, _P, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
 }

@@ -213,8 +213,7 @@ class Linear(torch.nn.Module):
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, nps,
             _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream(part)),
             "linear_bwd_w")
-        from .ops import sum_rows
-        return sum_rows(part)
+        return part.sum(0)
 
     def _bwd_bias(self, gy):
         parts = [gy[:, self._out_off[o]: self._out_off[o] + self.irreps_out[o].mul].sum(0)

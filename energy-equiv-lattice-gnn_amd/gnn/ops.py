@@ -84,18 +84,6 @@ def _i32(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.int32).contiguous()
 
 
-def sum_rows(part: torch.Tensor) -> torch.Tensor:
-    """``part.sum(0)`` of a contiguous fp32 partial buffer [rows, ...] on the HIP column-sum
-    kernel (rows added in order: deterministic)."""
-    part = _f32(part)
-    out = torch.empty(part.shape[1:], device=part.device, dtype=torch.float32)
-    rows = part.shape[0]
-    width = out.numel()
-    _lib.check(_lib.load().eelg_sum_rows(_lib.ptr(part), rows, width, _lib.ptr(out),
-                                         _lib.stream(out)), "sum_rows")
-    return out
-
-
 # ---------------------------------------------------------------------------
 # edge graph in receiver-sorted order
 # ---------------------------------------------------------------------------
@@ -374,7 +362,7 @@ class _SymCon(torch.autograd.Function):
                 _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul,
                                                 chunk, _lib.ptr(part), _lib.stream(part)), "sc_bwd_coef")
                 TIMER.stop(tok)
-                gcoef = sum_rows(part)
+                gcoef = part.sum(0)
         return gx, gcoef, None, None, None, None
 
 
@@ -476,12 +464,12 @@ class _RadialMLP(torch.autograd.Function):
                                        ctypes.byref(d), _lib.ptr(params[-1]), _lib.ptr(zsave),
                                        _lib.ptr(feats), _lib.ptr(grad_h), _lib.ptr(part_h),
                                        _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
-        small = sum_rows(part_h)
+        small = part_h.sum(0)
         grads, off = [], 0
         for p in params[:-1]:
             grads.append(small[off: off + p.numel()].view_as(p))
             off += p.numel()
-        grads.append(sum_rows(part_wo))
+        grads.append(part_wo.sum(0))
         return (None, None, *grads)
 
 

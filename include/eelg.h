@@ -99,12 +99,6 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
                            const float* row_scale, float scale, int n_rows, int width, int n_split,
                            float* work, float* out, void* stream);
 
-/* Column sums out[w] = sum_r src[r, w] of a [rows, width] row-major block, rows in order
- * (deterministic): the caller-side sum of the per-slice / per-chunk partials that the
- * weight-gradient kernels below write (eelg_linear_bwd_w, eelg_sc_bwd_coef, eelg_radial_bwd),
- * i.e. the reduction autograd performs for the reference's weight gradients. */
-int eelg_sum_rows(const float* src, int rows, int width, float* out, void* stream);
-
 /* Crystal-graph edge convolution (CGC/mCGC benchmark models): replaces
  *   c = cat([x[sender], x[receiver], edge_ft]); msg = softplus(fc_values(c)) * sigmoid(fc_multip(c));
  *   scatter(msg, receiver, reduce)          (scripts/benchmark_models/cgc_modified.py:20-25,

@@ -392,18 +392,6 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
     assert rel_err(got, want) < 1e-5
 
 
-@pytest.mark.parametrize("rows,width", [(49, 43040), (64, 240608), (1, 7), (3, 5), (0, 8), (186, 86016)])
-def test_sum_rows_matches_torch(rows, width):
-    """eelg_sum_rows (the weight-gradient partial sums) against torch.sum in fp64."""
-    from gnn import ops
-    torch.manual_seed(rows + width)
-    part = torch.randn(rows, width, device=DEV)
-    got = ops.sum_rows(part)
-    want = part.double().sum(0)
-    assert got.shape == (width,)
-    assert float((got.double() - want).abs().max()) <= 1e-5 * max(1.0, float(want.abs().max()))
-
-
 @pytest.mark.parametrize("irreps", ["32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+16x0e+32x1o"])
 def test_linear_residual_epilogue(irreps):
     """Linear(x, residual) == Linear(x) + residual in value and in every gradient (the fused
