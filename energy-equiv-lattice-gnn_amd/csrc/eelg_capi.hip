@@ -460,10 +460,31 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
       const int g = (n_nodes + nb - 1) / nb;
       max_groups = g > max_groups ? g : max_groups;
     }
+    const int gpw = lin_jl_gpw();
+    if (gpw > 0 && lin_fwd_jl_ok(desc)) {
+      const int gbj = (max_groups + LINF_WAVES * gpw - 1) / (LINF_WAVES * gpw);
+      dim3 grid(((gbj + 7) / 8) * 8, desc->n_slots, 1);
+      hipLaunchKernelGGL(lin_fwd_fast_jl_kernel, grid, dim3(64 * LINF_WAVES), 0, (hipStream_t)stream,
+                         x, x_row, w, bias, n_nodes, y, y_row, *desc, res, gpw);
+      return check_launch("linear_fwd");
+    }
     const int gblocks = (max_groups + LINF_WAVES * LINF_GPW - 1) / (LINF_WAVES * LINF_GPW);
     dim3 grid(((gblocks + 7) / 8) * 8 * desc->max_jt, desc->n_slots, 1);
-    hipLaunchKernelGGL(lin_fwd_fast_kernel, grid, dim3(64 * LINF_WAVES), 0, (hipStream_t)stream, x,
-                       x_row, w, bias, n_nodes, y, y_row, *desc, res);
+    int ws4;
+    size_t lds;
+    lin_fwd_fast_lds(desc, &ws4, &lds);
+    // one column tile per slot (the 800 -> 800 linears): two workgroups per CU measured faster
+    if (desc->max_jt == 1 && lds < lin_lds_1jt()) lds = lin_lds_1jt();
+    if (lds < lin_lds_floor()) lds = lin_lds_floor();
+    static bool lds_attr = false;   // > 64 KB of dynamic LDS must be allowed explicitly
+    if (!lds_attr) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return fail(-3, "linear_fwd: cannot raise the dynamic LDS limit");
+      lds_attr = true;
+    }
+    hipLaunchKernelGGL(lin_fwd_fast_kernel, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream, x,
+                       x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
     return check_launch("linear_fwd");
   }
   dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, 1);  // column tiles loop in-kernel
