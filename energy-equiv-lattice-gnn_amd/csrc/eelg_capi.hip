@@ -473,6 +473,26 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
     int ws4;
     size_t lds;
     lin_fwd_fast_lds(desc, &ws4, &lds);
+    if (desc->max_jt == 1 && lin_bal_rounds() > 0) {
+      // balanced persistent form: one workgroup per resident slot (LDS- or VGPR-limited)
+      if (lds < lin_lds_floor()) lds = lin_lds_floor();
+      static bool bal_attr = false;
+      if (!bal_attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_bal_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+          return fail(-3, "linear_fwd: cannot raise the dynamic LDS limit");
+        bal_attr = true;
+      }
+      int per_cu = (int)((160 * 1024) / lds);
+      if (per_cu > LINF_BAL_MAXWG) per_cu = LINF_BAL_MAXWG;
+      if (per_cu < 1) per_cu = 1;
+      eelg_lin_bal_plan plan;
+      lin_bal_plan(desc, n_nodes, 256 * per_cu * lin_bal_rounds(), &plan);
+      hipLaunchKernelGGL(lin_fwd_bal_kernel, dim3(plan.wg_end[desc->n_slots - 1]), dim3(64 * LINF_WAVES),
+                         lds, (hipStream_t)stream, x, x_row, w, bias, n_nodes, y, y_row, *desc, res,
+                         ws4, plan);
+      return check_launch("linear_fwd");
+    }
     // one column tile per slot (the 800 -> 800 linears): two workgroups per CU measured faster
     if (desc->max_jt == 1 && lds < lin_lds_1jt()) lds = lin_lds_1jt();
     if (lds < lin_lds_floor()) lds = lin_lds_floor();

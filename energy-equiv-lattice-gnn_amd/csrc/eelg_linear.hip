@@ -523,17 +523,15 @@ template <int D>
 __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
                                              const float* __restrict__ bias, int n_nodes,
                                              float* __restrict__ y, int y_row,
-                                             const eelg_lin_slot& sl, int gb, int jt,
-                                             const float* __restrict__ ws, float* __restrict__ xw,
-                                             const float* __restrict__ res) {
+                                             const eelg_lin_slot& sl, int g_base, int g_lim,
+                                             int jt, const float* __restrict__ ws,
+                                             float* __restrict__ xw, const float* __restrict__ res) {
+  // this wave's node groups: g_base + wave, g_base + wave + LINF_WAVES, ... < g_lim
   using G = LinfGeom<D>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
-  const int n_groups = (n_nodes + G::NB - 1) / G::NB;
-  const int g_base = gb * LINF_WAVES * LINF_GPW;
   int nch = 0;
   for (int s = 0; s < sl.n_src; ++s) nch += sl.src[s].k / 32;
-  int my_groups = 0;
-  for (int k = 0; k < LINF_GPW; ++k) my_groups += (g_base + k * LINF_WAVES + wave < n_groups);
+  const int my_groups = g_base + wave < g_lim ? (g_lim - g_base - wave + LINF_WAVES - 1) / LINF_WAVES : 0;
   const int nq = my_groups * nch;
   if (nq == 0) return;
   // this lane's operand row
@@ -630,6 +628,21 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
     }
   } else {
     for (int q = 0; q < nq; ++q) step(q, ra);
+  }
+}
+
+__device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ x, int x_row,
+                                               const float* __restrict__ bias, int n_nodes,
+                                               float* __restrict__ y, int y_row,
+                                               const eelg_lin_slot& sl, int g0, int g1, int jt,
+                                               const float* __restrict__ ws, float* __restrict__ xw,
+                                               const float* __restrict__ res) {
+  switch (d) {
+    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
   }
 }
 
@@ -810,12 +823,62 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   }
   __syncthreads();
   float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
-  switch (d) {
-    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
-    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
-    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
-    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
-    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, gb, jt, ws, xw, res); break;
+  const int g0 = gb * LINF_WAVES * LINF_GPW, g1 = min(n_groups, g0 + LINF_WAVES * LINF_GPW);
+  lin_fwd_fast_d(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
+}
+
+// Balanced form for one column tile per slot (the 7360 -> 800 and 800 -> 800 linears): the
+// grid is sized to the resident workgroups and split over the slots in proportion to their
+// cost (node groups x K chunks; plan.wg_end = the running workgroup counts, slots heavy
+// first); a slot's workgroups take equal contiguous ranges of its node groups.  No partially
+// filled last round of workgroups, and the weight tile is staged once per workgroup instead
+// of once per 32 node groups.
+struct eelg_lin_bal_plan { int wg_end[EELG_LIN_MAXSLOT]; };
+
+__global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_bal_kernel(
+    const float* __restrict__ x, int x_row, const float* __restrict__ w,
+    const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
+    eelg_lin_desc desc, const float* __restrict__ res, int ws4, eelg_lin_bal_plan plan) {
+  extern __shared__ float4 linf_smem[];
+  float* ws = reinterpret_cast<float*>(linf_smem);
+  float* xw = reinterpret_cast<float*>(linf_smem + ws4) + (threadIdx.x >> 6) * LINF_XW;
+  int o = 0;
+  while (o + 1 < desc.n_slots && (int)blockIdx.x >= plan.wg_end[o]) ++o;
+  const int wg0 = o ? plan.wg_end[o - 1] : 0, nwg = plan.wg_end[o] - wg0, j = blockIdx.x - wg0;
+  const eelg_lin_slot& sl = desc.slot[desc.n_slots - 1 - o];
+  const int ng = (n_nodes + 32 / sl.d - 1) / (32 / sl.d);
+  const int g0 = (int)((long long)ng * j / nwg), g1 = (int)((long long)ng * (j + 1) / nwg);
+  if (g0 >= g1) return;   // uniform per workgroup
+  int kb = 0;
+  for (int t = 0; t < sl.n_src; ++t) {
+    const eelg_lin_src& src = sl.src[t];
+    for (int e = threadIdx.x; e < src.k * 32; e += 64 * LINF_WAVES) {
+      const int k = e >> 5, jj = e & 31;
+      ws[(kb + k) * 32 + jj] = w[src.w_off + (size_t)k * src.ldk + (size_t)jj * src.ldj] * src.alpha;
+    }
+    kb += src.k;
+  }
+  __syncthreads();
+  lin_fwd_fast_d(sl.d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, 0, ws, xw, res);
+}
+
+// workgroups per slot (slots heavy first) for lin_fwd_bal_kernel: proportional to cost
+static void lin_bal_plan(const eelg_lin_desc* desc, int n_nodes, int total_wg, eelg_lin_bal_plan* p) {
+  long long cost[EELG_LIN_MAXSLOT], total = 0;
+  for (int o = 0; o < desc->n_slots; ++o) {
+    const eelg_lin_slot& sl = desc->slot[desc->n_slots - 1 - o];
+    int nch = 0;
+    for (int t = 0; t < sl.n_src; ++t) nch += sl.src[t].k / 32;
+    cost[o] = (long long)((n_nodes + 32 / sl.d - 1) / (32 / sl.d)) * nch;
+    total += cost[o];
+  }
+  long long acc = 0;
+  int prev = 0;
+  for (int o = 0; o < desc->n_slots; ++o) {
+    acc += cost[o];
+    int e = (int)((acc * total_wg + total / 2) / (total > 0 ? total : 1));
+    if (e < prev + 1) e = prev + 1;   // every slot gets a workgroup
+    p->wg_end[o] = prev = e;
   }
 }
 
@@ -840,6 +903,24 @@ static size_t lin_lds_1jt() {   // EELG_LINF_LDS_1JT overrides LINF_LDS_1JT
     if (v < 0) v = 0;
   }
   return (size_t)v;
+}
+#ifndef LINF_BAL_MAXWG
+#define LINF_BAL_MAXWG 3           // resident 8-wave workgroups per CU (VGPR-limited at <= 85 VGPRs)
+#endif
+#ifndef LINF_BAL_ROUNDS
+#define LINF_BAL_ROUNDS 0   // off: 1 and 4 measured slower in the training step (r02 ab_bal2)
+#endif
+// EELG_LIN_BAL: workgroups of the balanced grid in units of the resident count (0: the
+// one-workgroup-per-32-groups grid).  Side-stream kernels share the CUs in the training step,
+// so a grid of exactly the resident count leaves a tail behind the slowest CU.
+static int lin_bal_rounds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EELG_LIN_BAL");
+    v = e ? atoi(e) : LINF_BAL_ROUNDS;
+    if (v < 0) v = 0;
+  }
+  return v;
 }
 // weight region (float4) and total dynamic LDS bytes of lin_fwd_fast_kernel for a descriptor
 static void lin_fwd_fast_lds(const eelg_lin_desc* desc, int* ws4, size_t* bytes) {
