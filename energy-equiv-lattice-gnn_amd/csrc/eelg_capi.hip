@@ -242,7 +242,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
-  info[5] = c.Dout; info[6] = c.nbc; info[7] = c.coef_mm;
+  info[5] = c.Dout; info[6] = c.nbc; info[7] = c.coef_mm; info[8] = c.fwd_cp;
   *sig = c.sig;
   return 0;
 }
@@ -390,7 +390,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
+  hipLaunchKernelGGL(c->fwd, dim3(mul / (c->fwd_cp ? 8 : 4), (n_nodes + (c->fwd_cp ? 64 : c->nb) - 1) / (c->fwd_cp ? 64 : c->nb)), dim3(256), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }

@@ -49,6 +49,10 @@ TP_UNROLL2 = int(os.environ.get("EELG_TP_UNROLL2", "0"))
 # 0.86): twice the VGPRs and LDS per workgroup halve the occupancy, the SGPR coefficient
 # operands need aligned pairs (s_mov per term), and dependent v_pk ops carry a wait state
 SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+# forward with two channels per lane (packed fp32: v_pk_mul / v_pk_fma with a channel-pair
+# coefficient in one SGPR pair); the coefficients are then read channel-pair interleaved
+SC_FWD_CP = int(os.environ.get("EELG_SC_FWD_CP", "0"))
+SC_CP_MAXB = int(os.environ.get("EELG_SC_CP_MAXB", "16"))
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, forward / grad-x (r02: grad-x 0.56 -> 0.51 ms at 3; the forward spills SGPRs at 2+)
 SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
@@ -715,8 +719,9 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     Q = 4                                   # channels per workgroup
 
     class Lay:
-        """per-channel component list of one row layout"""
-        def __init__(self, irreps, tag):
+        """per-channel component list of one row layout (q channels per workgroup tile)"""
+        def __init__(self, irreps, tag, q=4):
+            Q = q
             self.comp, off, seg = [], 0, 0   # component a -> (l, m, row offset, seg start)
             self.segs = []
             for ir in irreps:
@@ -846,56 +851,156 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
             f"  const float* __restrict__ cf = coef + (size_t)c * {nt};"]
 
     # ---------------- forward ----------------
-    L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
-    L.append("    float* __restrict__ out) {")
-    L.append(f"  __shared__ float tile[{NB} * {TP}];")
-    L += head
-    L += stage_in("x", "tile", lin, NB)
-    L.append("  __syncthreads();")
-    # packed: a lane owns nodes n0 + lane and n0 + 64 + lane (one v_pk_* op covers both)
-    L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
-    if PKN == 2:
-        L.append(f"  float* __restrict__ tr1 = tile + (lane + 64) * {TP};")
-    for a in range(D):
-        L.append("  " + ld_pair(f"x{a}", "tr", "tr1", lq(lin, a, 'cl')))
-    for q in range(Dout):
-        L.append(f"  {FT} o{q} = {ZERO};")
-    blocks = sc_blocks(plan)
-    fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    for b0 in blocks[:SC_PFD_FWD]:
-        for t in b0["terms"]:
-            L.append(f"  float c{t} = cf[{t}];")
-    for bi, blk in enumerate(blocks):
-        # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
-        for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
-            L.append(f"  float c{t} = cf[{t}];")
-        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
-        carry = []
-        if blk["kind"] == "deg1":
-            for t, a, q in blk["deg1"]:
-                L.append(f"  o{q} = {fma_s(f'c{t}', f'x{a}', f'o{q}')};")
-        else:
-            a, b = blk["a"], blk["b"]
-            pv = f"p{a}_{b}"
-            if blk["first"]:
-                L.append(f"  {FT} {pv} = x{a} * x{b};")
-            for t, q in blk["d2"]:
-                L.append(f"  o{q} = {fma_s(f'c{t}', pv, f'o{q}')};")
-            for cc, lst in blk["d3"]:
-                L.append(f"  {{ const {FT} m = {pv} * x{cc};")
-                for t, q in lst:
-                    L.append(f"    o{q} = {fma_s(f'c{t}', 'm', f'o{q}')};")
-                L.append("  }")
-            if not blk["last"]:
-                carry = [pv]
-        L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
-    L.append("  __syncthreads();")
-    for q in range(Dout):
-        L.append("  " + st_pair(f"o{q}", "tr", "tr1", lq(lout, q, 'cl')))
-    L.append("  __syncthreads();")
-    L += stage_out("out", "tile", lout, NB)
-    L.append("}")
+    if not SC_FWD_CP:
+        L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
+        L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
+        L.append("    float* __restrict__ out) {")
+        L.append(f"  __shared__ float tile[{NB} * {TP}];")
+        L += head
+        L += stage_in("x", "tile", lin, NB)
+        L.append("  __syncthreads();")
+        # packed: a lane owns nodes n0 + lane and n0 + 64 + lane (one v_pk_* op covers both)
+        L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
+        if PKN == 2:
+            L.append(f"  float* __restrict__ tr1 = tile + (lane + 64) * {TP};")
+        for a in range(D):
+            L.append("  " + ld_pair(f"x{a}", "tr", "tr1", lq(lin, a, 'cl')))
+        for q in range(Dout):
+            L.append(f"  {FT} o{q} = {ZERO};")
+        blocks = sc_blocks(plan)
+        fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
+        for b0 in blocks[:SC_PFD_FWD]:
+            for t in b0["terms"]:
+                L.append(f"  float c{t} = cf[{t}];")
+        for bi, blk in enumerate(blocks):
+            # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
+            for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
+                L.append(f"  float c{t} = cf[{t}];")
+            nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
+            carry = []
+            if blk["kind"] == "deg1":
+                for t, a, q in blk["deg1"]:
+                    L.append(f"  o{q} = {fma_s(f'c{t}', f'x{a}', f'o{q}')};")
+            else:
+                a, b = blk["a"], blk["b"]
+                pv = f"p{a}_{b}"
+                if blk["first"]:
+                    L.append(f"  {FT} {pv} = x{a} * x{b};")
+                for t, q in blk["d2"]:
+                    L.append(f"  o{q} = {fma_s(f'c{t}', pv, f'o{q}')};")
+                for cc, lst in blk["d3"]:
+                    L.append(f"  {{ const {FT} m = {pv} * x{cc};")
+                    for t, q in lst:
+                        L.append(f"    o{q} = {fma_s(f'c{t}', 'm', f'o{q}')};")
+                    L.append("  }")
+                if not blk["last"]:
+                    carry = [pv]
+            L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  __syncthreads();")
+        for q in range(Dout):
+            L.append("  " + st_pair(f"o{q}", "tr", "tr1", lq(lout, q, 'cl')))
+        L.append("  __syncthreads();")
+        L += stage_out("out", "tile", lout, NB)
+        L.append("}")
+
+    else:
+        # two channels per lane (v_pk_* fp32): a workgroup of 4 waves owns 8 channels x 64
+        # nodes; wave w holds channels 2w, 2w+1 of every node in one register pair, and the
+        # coefficients come channel-pair interleaved (cf2[t] = {coef[c0][t], coef[c0+1][t]}),
+        # one SGPR pair per term
+        l8, o8 = Lay(irs, "in8", 8), Lay(out_irs, "out8", 8)
+        if o8.comp == l8.comp:
+            o8.goff = l8.goff
+        T8 = max(l8.QD, o8.QD) + 1
+        if T8 % 2 == 0:
+            T8 += 1
+        for lay in ((l8,) if o8.comp == l8.comp else (l8, o8)):
+            L.append(f"__device__ __forceinline__ int {lay.goff}(int q, int cq) {{")
+            for (sa, sb, so, sd) in lay.segs[:-1]:
+                L.append(f"  if (q < {sb}) return {so} + cq * {8 * sd} + (q - {sa});")
+            sa, sb, so, sd = lay.segs[-1]
+            L.append(f"  return {so} + cq * {8 * sd} + (q - {sa});")
+            L.append("}")
+
+        def st_in8(src, lay):
+            per = (64 * lay.QD + 255) // 256
+            return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
+                    "#pragma unroll 2",
+                    f"  for (int it = 0; it < {per}; ++it) {{",
+                    "    const int idx = tid + 256 * it;",
+                    f"    if (idx < {64 * lay.QD}) {{",
+                    f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
+                    f"      tile[nl * {T8} + q] = (n < n_nodes) ? {src}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] : 0.0f;",
+                    "    }", "  } }"]
+
+        def st_out8(dst, lay):
+            per = (64 * lay.QD + 255) // 256
+            return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
+                    "#pragma unroll 2",
+                    f"  for (int it = 0; it < {per}; ++it) {{",
+                    "    const int idx = tid + 256 * it;",
+                    f"    if (idx < {64 * lay.QD}) {{",
+                    f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
+                    f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = tile[nl * {T8} + q];",
+                    "    }", "  } }"]
+
+        def lq8(lay, a_, cl):
+            l_, m_, _, sg = lay.comp[a_]
+            return f"{sg} + ({cl}) * {2 * l_ + 1} + {m_}"
+
+        L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
+        L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
+        L.append("    float* __restrict__ out) {")
+        L.append(f"  __shared__ float tile[64 * {T8}];")
+        L.append("  const int cq = blockIdx.x;   // channel octet")
+        L.append("  const int n0 = blockIdx.y * 64;")
+        L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
+        L.append("  const int cp = __builtin_amdgcn_readfirstlane(cq * 4 + wv);   // channel pair")
+        L.append(f"  const float* __restrict__ cf = coef + (size_t)cp * {2 * nt};")
+        L += st_in8("x", l8)
+        L.append("  __syncthreads();")
+        L.append(f"  float* __restrict__ tr = tile + lane * {T8};")
+        for a_ in range(D):
+            L.append(f"  eelg_f2 x{a_} = eelg_f2{{tr[{lq8(l8, a_, '2 * wv')}], tr[{lq8(l8, a_, '2 * wv + 1')}]}};")
+        for q in range(Dout):
+            L.append(f"  eelg_f2 o{q} = eelg_f2{{0.0f, 0.0f}};")
+        blocks = sc_blocks(plan, SC_CP_MAXB)
+        fv = [f"x{a_}" for a_ in range(D)] + [f"o{q}" for q in range(Dout)]
+
+        def cload(t):
+            return f"  eelg_f2 c{t} = *reinterpret_cast<const eelg_f2*>(cf + {2 * t});"
+        for b0 in blocks[:SC_PFD_FWD]:
+            for t in b0["terms"]:
+                L.append(cload(t))
+        for bi, blk in enumerate(blocks):
+            for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
+                L.append(cload(t))
+            nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
+            carry = []
+            if blk["kind"] == "deg1":
+                for t, a_, q in blk["deg1"]:
+                    L.append(f"  o{q} = eelg_fma2(c{t}, x{a_}, o{q});")
+            else:
+                a_, b_ = blk["a"], blk["b"]
+                pv = f"p{a_}_{b_}"
+                if blk["first"]:
+                    L.append(f"  eelg_f2 {pv} = x{a_} * x{b_};")
+                for t, q in blk["d2"]:
+                    L.append(f"  o{q} = eelg_fma2(c{t}, {pv}, o{q});")
+                for cc, lst in blk["d3"]:
+                    L.append(f"  {{ const eelg_f2 m = {pv} * x{cc};")
+                    for t, q in lst:
+                        L.append(f"    o{q} = eelg_fma2(c{t}, m, o{q});")
+                    L.append("  }")
+                if not blk["last"]:
+                    carry = [pv]
+            L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  __syncthreads();")
+        for q in range(Dout):
+            L.append(f"  tr[{lq8(o8, q, '2 * wv')}] = o{q}.x; tr[{lq8(o8, q, '2 * wv + 1')}] = o{q}.y;")
+        L.append("  __syncthreads();")
+        L += st_out8("out", o8)
+        L.append("}")
 
     # ---------------- backward w.r.t. x ----------------
     L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
@@ -1122,7 +1227,7 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     L.append("}")
     WPB, NBC = WV, NCB
     info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
-                coef_mulmajor=SC_COEF_MULMAJOR,
+                coef_mulmajor=SC_COEF_MULMAJOR, fwd_cp=SC_FWD_CP,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -1175,7 +1280,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}, {i["coef_mulmajor"]}}},')
+                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}, {i["coef_mulmajor"]}, {i["fwd_cp"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -165,12 +165,13 @@ def _tp_info(idx: int):
 
 
 def _sc_info(idx: int):
-    info = (ctypes.c_int * 8)()
+    info = (ctypes.c_int * 9)()
     sig = ctypes.c_uint64()
     rc = load().eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P))
     if rc != 0:
         return None
-    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk", "coef_mulmajor")
+    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk", "coef_mulmajor",
+            "coef_pairs")
     return dict(zip(keys, list(info))), sig.value
 
 

@@ -290,8 +290,11 @@ class _SymCon(torch.autograd.Function):
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
         out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
+        # two-channels-per-lane forward: coefficients channel-pair interleaved [mul/2, nt, 2]
+        cf = (coef.view(mul // 2, 2, -1).transpose(1, 2).contiguous()
+              if info.get("coef_pairs", 0) else coef)
         tok = TIMER.start("sc_fwd")
-        _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),
+        _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(cf), n, mul, _lib.ptr(out),
                                    _lib.stream(out)), "sc_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, coef)

@@ -36,13 +36,16 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk, coef_mulmajor}
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk, coef_mulmajor,
+ * coef_pairs}
  * (D: coupling components per channel of the input, D_out: of the output; they differ when the
  * product maps the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node
  * chunk of eelg_sc_bwd_coef; coef_mulmajor: 1 if eelg_sc_bwd_coef takes the mul-major x /
- * grad_out rows, 0 if it takes the channel-major copies of eelg_sc_bwd_x_cm) */
+ * grad_out rows, 0 if it takes the channel-major copies of eelg_sc_bwd_x_cm; coef_pairs: 1 if
+ * eelg_sc_fwd takes the coefficients channel-pair interleaved, coef2[c/2][t][c%2], 0 if
+ * [mul][nterms] like eelg_sc_bwd_x) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info8, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info9, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -125,7 +128,8 @@ int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_row
 
 /* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
  * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
- * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms]. */
+ * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms], or channel-pair interleaved
+ * [mul/2][nterms][2] for eelg_sc_fwd when the config's coef_pairs (eelg_sc_info info[8]) is 1. */
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
