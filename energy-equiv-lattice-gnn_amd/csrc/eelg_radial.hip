@@ -28,6 +28,7 @@
 //   radial_bwd_wo   : grad W_o = grad_w^T h_NH per (128-column block, edge split),
 //                     h_NH = SiLU(z) staged once per workgroup in LDS for its 4 waves
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "../../include/eelg.h"
@@ -559,6 +560,21 @@ static int radial_check(const eelg_radial_desc* d, int n_edges) {
     else { if (bf) hipLaunchKernelGGL((KERNEL<32, 3, true>), GRID, dim3(256), 0, st, __VA_ARGS__); else hipLaunchKernelGGL((KERNEL<32, 3, false>), GRID, dim3(256), 0, st, __VA_ARGS__); } \
   } while (0)
 
+#ifndef RAD_WO_WG
+#define RAD_WO_WG 1024
+#endif
+// EELG_RAD_WO_WG overrides the target workgroup count of radial_bwd_wo (each edge split leaves
+// one [W, H] partial that the host sums)
+static int rad_wo_wg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("EELG_RAD_WO_WG");
+    v = e ? atoi(e) : RAD_WO_WG;
+    if (v < 1) v = RAD_WO_WG;
+  }
+  return v;
+}
+
 // launch plan shared by the host (partial-buffer sizes) and the launches below
 static void radial_plan(int n_edges, int n_out, int* n_part, int* n_split, int* tiles_per_split) {
   const int ntile = (n_edges + 31) / 32;
@@ -567,7 +583,8 @@ static void radial_plan(int n_edges, int n_out, int* n_part, int* n_split, int* 
   if (wg < 1) wg = 1;
   *n_part = wg;
   const int ncb = (n_out + 127) / 128;
-  int s = (2048 + ncb - 1) / ncb;   // ~2048 workgroups for the output-weight gradient
+  const int wo_wg = rad_wo_wg();
+  int s = (wo_wg + ncb - 1) / ncb;  // ~RAD_WO_WG workgroups for the output-weight gradient
   if (s > ntile) s = ntile;
   if (s < 1) s = 1;
   const int tps = (ntile + s - 1) / s;

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from collections import Counter
 from typing import List, Tuple
 
@@ -19,6 +20,10 @@ import torch
 
 from . import cg
 from .irreps import Irreps
+
+# grad-W launch shape: target workgroups and a cap on the node slices (partials)
+LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
+LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "1000000"))
 
 
 def _accept_output_mask(state_dict, key: str, irreps_out, covered, error_msgs) -> None:
@@ -203,8 +208,9 @@ class Linear(torch.nn.Module):
         n = x.shape[0]
         if not self.instructions:
             return torch.zeros_like(self.weight)
-        # ~2048 workgroups in total: (node slices) x (32x32 weight tiles of all instructions)
-        slices = max(1, min((n + 31) // 32, -(-2048 // self._bw_tiles)))
+        # ~LINW_WG workgroups in total: (node slices) x (32x32 weight tiles of all
+        # instructions); each slice leaves one partial weight gradient that the sum reads back
+        slices = max(1, min((n + 31) // 32, -(-LINW_WG // self._bw_tiles), LINW_MAX_SLICES))
         nps = -(-n // slices)
         slices = -(-n // nps)
         self._bw_desc.max_rows = n * self._bw_maxd
