@@ -14,6 +14,7 @@ used by ``EnergyEquivGNN``).
 """
 from __future__ import annotations
 
+import os
 from argparse import Namespace
 from typing import Optional, Tuple, Union
 
@@ -23,7 +24,10 @@ import torch
 from . import _lib, cg, kernel_sets, ops
 from .irreps import Irreps
 from .mace import SymmetricContraction
-from .o3 import Gate, Linear, TensorProduct
+from .o3 import Gate, GradMailbox, Linear, TensorProduct
+
+# the layer residual's gradient summed in linear_up's grad-x epilogue (1) or by autograd (0)
+RESIDUAL_GRAD_FUSED = os.environ.get("EELG_RESIDUAL_GRAD_FUSED", "1") != "0"
 
 EdgeIndex = Union[torch.Tensor, ops.EdgeCSR]
 
@@ -144,10 +148,11 @@ class EquivariantProductBlock(torch.nn.Module):
         self.symmetric_contractions = SymmetricContraction(node_feats_irreps, sc_out, correlation)
         self.linear = Linear(sc_out, target_irreps)
 
-    def forward(self, node_feats, sc, residual: Optional[torch.Tensor] = None):
+    def forward(self, node_feats, sc, residual: Optional[torch.Tensor] = None, grad_mailbox=None):
         """``residual``: the model's layer residual (``gnn/model.py:95``), added in the linear's
         epilogue instead of by a separate pass."""
-        x = self.linear(self.symmetric_contractions(node_feats), residual=residual)
+        x = self.linear(self.symmetric_contractions(node_feats), residual=residual,
+                        grad_mailbox=grad_mailbox)
         return x + sc if self.use_sc else x
 
 
@@ -218,12 +223,12 @@ class TensorProductInteractionBlock(torch.nn.Module):
 
     def forward(self, node_feats, edge_attrs, edge_feats, edge_index: EdgeIndex,
                 node_attrs: Optional[torch.Tensor] = None,
-                tp_weights: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, None]:
+                tp_weights: Optional[torch.Tensor] = None, grad_mailbox=None) -> Tuple[torch.Tensor, None]:
         """``tp_weights``: ``radial_weights(edge_feats)`` computed ahead (possibly on another
         stream, see ``GNN_Head``); computed here when not given."""
         csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
         idx, info = self._config()
-        x = self.linear_up(node_feats)
+        x = self.linear_up(node_feats, grad_mailbox=grad_mailbox)
         w = self.radial_weights(edge_feats) if tp_weights is None else tp_weights
         agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
         return self.linear(agg), None
@@ -251,5 +256,9 @@ class MACELayer(torch.nn.Module):
         csr, edge_sh, edge_scalars = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_scalars)
         if tp_weights is not None and not isinstance(edge_index, ops.EdgeCSR):
             tp_weights = tp_weights[csr.perm]
-        node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr, tp_weights=tp_weights)
-        return self.product(node_ft, sc, residual=residual)
+        # the residual h is also linear_up's input: its two gradient contributions are summed
+        # in linear_up's grad-x epilogue (o3.GradMailbox), not by autograd in a separate pass
+        mb = GradMailbox() if (RESIDUAL_GRAD_FUSED and residual is node_ft) else None
+        node_ft, sc = self.interaction(node_ft, edge_sh, edge_scalars, csr, tp_weights=tp_weights,
+                                       grad_mailbox=mb)
+        return self.product(node_ft, sc, residual=residual, grad_mailbox=mb)

@@ -52,25 +52,42 @@ class _OnStream(torch.autograd.Function):
         return g, None
 
 
+class GradMailbox:
+    """Hands the layer residual's gradient from the linear that adds the residual (forward
+    ``residual=h``) to the linear that reads ``h`` first (``linear_up``), whose grad-x kernel
+    adds it in its epilogue: autograd would otherwise sum the two gradient contributions of
+    ``h`` in a separate pass over [N, 800].  Backward order is fixed by the data flow (the
+    residual's linear is downstream of ``linear_up``), so the deposit precedes the collection."""
+
+    def __init__(self):
+        self.grad = None
+
+
 class _IrrepsLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, lin: "Linear", side=None, residual=None):
+    def forward(ctx, x, weight, bias, lin: "Linear", side=None, residual=None, mailbox=None):
         ctx.save_for_backward(x, weight)
-        ctx.lin, ctx.side = lin, side
+        ctx.lin, ctx.side, ctx.mailbox = lin, side, mailbox
+        ctx.deposit = residual is not None
         return lin._fwd(x, weight, bias, residual)
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
-        lin, side = ctx.lin, ctx.side
+        lin, side, mb = ctx.lin, ctx.side, ctx.mailbox
         gy = gy.contiguous()
-        gx = lin._bwd_x(gy, weight) if ctx.needs_input_grad[0] else None
-        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         gres = gy if ctx.needs_input_grad[5] else None      # y = linear(x) + residual
+        if gres is not None and mb is not None:
+            mb.grad, gres = gres, None                      # added by the collecting linear
+        extra = None
+        if mb is not None and not ctx.deposit:
+            extra, mb.grad = mb.grad, None
+        gx = lin._bwd_x(gy, weight, extra) if ctx.needs_input_grad[0] else None
+        want_w, want_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         if side is None or not (want_w or want_b):
             gw = lin._bwd_w(x, gy) if want_w else None
             gb = lin._bwd_bias(gy) if want_b else None
-            return gx, gw, gb, None, None, gres
+            return gx, gw, gb, None, None, gres, None
         # weight / bias gradients on the side stream the parameters' views were made on:
         # their consumers (the views' backward, the accumulation) run there as well, and
         # the main stream carries on with grad-x
@@ -80,7 +97,7 @@ class _IrrepsLinearFn(torch.autograd.Function):
         with torch.cuda.stream(side):
             gw = lin._bwd_w(x, gy) if want_w else None
             gb = lin._bwd_bias(gy) if want_b else None
-        return gx, gw, gb, None, None, gres
+        return gx, gw, gb, None, None, gres, None
 
 
 class Linear(torch.nn.Module):
@@ -193,14 +210,21 @@ class Linear(torch.nn.Module):
             "linear_fwd")
         return y
 
-    def _bwd_x(self, gy, weight):
+    def _bwd_x(self, gy, weight, extra=None):
+        """grad-x; ``extra`` ([N, dim_in], e.g. a residual's gradient) is added in the epilogue"""
         from . import _lib
         n = gy.shape[0]
         gx = torch.empty(n, self.irreps_in.dim, device=gy.device, dtype=torch.float32)
         self._bx_desc.max_rows = n * self._bx_maxd
-        _lib.check(_lib.load().eelg_linear_fwd(
-            _lib.ptr(gy), self.irreps_out.dim, _lib.ptr(weight), None, n, _lib.ptr(gx),
-            self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream(gx)), "linear_bwd_x")
+        if extra is not None:
+            extra = extra.contiguous()
+            if extra.shape != gx.shape or extra.dtype != torch.float32:
+                raise ValueError(f"linear grad-x: added gradient {tuple(extra.shape)} does not "
+                                 f"match {tuple(gx.shape)}")
+        _lib.check(_lib.load().eelg_linear_fwd_res(
+            _lib.ptr(gy), self.irreps_out.dim, _lib.ptr(weight), None, _lib.ptr(extra), n,
+            _lib.ptr(gx), self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream(gx)),
+            "linear_bwd_x")
         return gx
 
     def _bwd_w(self, x, gy):
@@ -226,9 +250,12 @@ class Linear(torch.nn.Module):
                  for o in self.bias_slots]
         return torch.cat(parts)
 
-    def forward(self, x: torch.Tensor, residual: torch.Tensor = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: torch.Tensor = None,
+                grad_mailbox: "GradMailbox" = None) -> torch.Tensor:
         """``o3.Linear``; with ``residual`` returns ``linear(x) + residual`` with the add in the
-        kernel epilogue (the layer residual of ``gnn/model.py:92-96``)."""
+        kernel epilogue (the layer residual of ``gnn/model.py:92-96``).  ``grad_mailbox``
+        shared by the residual-adding linear and the first linear reading the residual moves
+        the residual's gradient into that linear's grad-x epilogue (``GradMailbox``)."""
         from .ops import _f32, _require_device
         _require_device(x)
         if x.shape[-1] != self.irreps_in.dim:
@@ -245,7 +272,7 @@ class Linear(torch.nn.Module):
         if residual is not None:
             _require_device(residual)
             residual = _f32(residual)
-        return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side, residual)
+        return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side, residual, grad_mailbox)
 
 
 class Gate(torch.nn.Module):
