@@ -127,6 +127,104 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Gate nonlinearity (readout): elementwise, one thread per output (fwd) / input (bwd) element
+// of a row, rows split over the grid; the gated block of an element is found by a walk over
+// the <= EELG_GATE_MAXBLK block offsets
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float gate_silu(float v) { return v / (1.0f + __expf(-v)); }
+__device__ __forceinline__ float gate_dsilu(float v) {
+  const float s = 1.0f / (1.0f + __expf(-v));
+  return s * (1.0f + v * (1.0f - s));
+}
+// element jj of the concatenated gated blocks -> (gate index within the gates, first element
+// of its (block, channel) run, run length d)
+__device__ __forceinline__ void gate_locate(const eelg_gate_desc& g, int jj, int& gi, int& r0, int& d) {
+  int off = 0, goff = 0;
+  for (int b = 0; b < g.n_blk; ++b) {
+    const int len = g.blk_mul[b] * g.blk_dim[b];
+    if (jj < off + len || b + 1 == g.n_blk) {
+      d = g.blk_dim[b];
+      const int u = (jj - off) / d;
+      gi = goff + u;
+      r0 = off + u * d;
+      return;
+    }
+    off += len;
+    goff += g.blk_mul[b];
+  }
+  gi = r0 = 0;
+  d = 1;
+}
+
+__global__ __launch_bounds__(256) void gate_fwd_kernel(const float* __restrict__ x, int n_nodes,
+                                                       eelg_gate_desc g, int din, int dout,
+                                                       float cst, float* __restrict__ y) {
+  for (int n = blockIdx.x; n < n_nodes; n += gridDim.x) {
+    const float* __restrict__ xr = x + (size_t)n * din;
+    float* __restrict__ yr = y + (size_t)n * dout;
+    for (int j = threadIdx.x; j < dout; j += 256) {
+      if (j < g.n_scal) {
+        yr[j] = cst * gate_silu(xr[j]);
+      } else {
+        const int jj = j - g.n_scal;
+        int gi, r0, d;
+        gate_locate(g, jj, gi, r0, d);
+        yr[j] = xr[g.n_scal + g.n_gates + jj] * (cst * gate_silu(xr[g.n_scal + gi]));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gate_bwd_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ gy, int n_nodes,
+                                                       eelg_gate_desc g, int din, int dout,
+                                                       float cst, float* __restrict__ gx) {
+  for (int n = blockIdx.x; n < n_nodes; n += gridDim.x) {
+    const float* __restrict__ xr = x + (size_t)n * din;
+    const float* __restrict__ gr = gy + (size_t)n * dout;
+    float* __restrict__ o = gx + (size_t)n * din;
+    const int gated0 = g.n_scal + g.n_gates;
+    for (int i = threadIdx.x; i < din; i += 256) {
+      const float v = xr[i];
+      if (i < g.n_scal) {
+        o[i] = gr[i] * cst * gate_dsilu(v);
+      } else if (i < gated0) {
+        // gate of (block b, channel u): sum over the run it scales of grad_y * x
+        const int gi = i - g.n_scal;
+        int off = 0, goff = 0, b = 0;
+        while (b + 1 < g.n_blk && gi >= goff + g.blk_mul[b]) { off += g.blk_mul[b] * g.blk_dim[b]; goff += g.blk_mul[b]; ++b; }
+        const int d = g.blk_dim[b], r0 = off + (gi - goff) * d;
+        float s = 0.0f;
+        for (int m = 0; m < d; ++m) s = fmaf(gr[g.n_scal + r0 + m], xr[gated0 + r0 + m], s);
+        o[i] = s * cst * gate_dsilu(v);
+      } else {
+        const int jj = i - gated0;
+        int gi, r0, d;
+        gate_locate(g, jj, gi, r0, d);
+        o[i] = gr[g.n_scal + jj] * (cst * gate_silu(xr[g.n_scal + gi]));
+      }
+    }
+  }
+}
+
+static int gate_check(const eelg_gate_desc* g, int* din, int* dout) {
+  if (!g || g->n_scal < 0 || g->n_blk < 0 || g->n_blk > EELG_GATE_MAXBLK)
+    return fail(-2, "gate: bad descriptor");
+  int gates = 0, len = 0;
+  for (int b = 0; b < g->n_blk; ++b) {
+    if (g->blk_mul[b] <= 0 || g->blk_dim[b] <= 0) return fail(-2, "gate: bad gated block %d", b);
+    gates += g->blk_mul[b];
+    len += g->blk_mul[b] * g->blk_dim[b];
+  }
+  if (gates != g->n_gates) return fail(-2, "gate: %d gates for %d gated channels", g->n_gates, gates);
+  *din = g->n_scal + g->n_gates + len;
+  *dout = g->n_scal + len;
+  return 0;
+}
+
+static int gate_grid(int n_nodes) { return n_nodes < 8192 ? n_nodes : 8192; }
+
 // Few long segments (graph pooling: 32 graphs x 1024 nodes): split each segment into
 // n_split contiguous pieces, one wave per (segment, piece) -> work[seg][piece][:], then
 // a fixed-order combine.  Deterministic, no atomics.
@@ -383,6 +481,26 @@ static const eelg_sc_cfg* sc_get(int cfg, int mul) {
   if (cfg < 0 || cfg >= n) { fail(-1, "bad sc config %d", cfg); return nullptr; }
   if (mul != 32) { fail(-2, "symmetric contraction built for mul=32, got %d", mul); return nullptr; }
   return &t[cfg];
+}
+
+int eelg_gate_fwd(const float* x, int n_nodes, const eelg_gate_desc* desc, float cst, float* y,
+                  void* stream) {
+  int din, dout;
+  if (int rc = gate_check(desc, &din, &dout)) return rc;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(gate_fwd_kernel, dim3(gate_grid(n_nodes)), dim3(256), 0, (hipStream_t)stream,
+                     x, n_nodes, *desc, din, dout, cst, y);
+  return check_launch("gate_fwd");
+}
+
+int eelg_gate_bwd(const float* x, const float* grad_y, int n_nodes, const eelg_gate_desc* desc,
+                  float cst, float* grad_x, void* stream) {
+  int din, dout;
+  if (int rc = gate_check(desc, &din, &dout)) return rc;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(gate_grid(n_nodes)), dim3(256), 0, (hipStream_t)stream,
+                     x, grad_y, n_nodes, *desc, din, dout, cst, grad_x);
+  return check_launch("gate_bwd");
 }
 
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,

@@ -35,6 +35,8 @@ _SIGS = {
     "eelg_segment_sum_csr": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_csr_bf16": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_split": ([_P, _P, _P, _P, _F, _I, _I, _I, _P, _P, _P], _I),
+    "eelg_gate_fwd": ([_P, _I, _P, _F, _P, _P], _I),
+    "eelg_gate_bwd": ([_P, _P, _I, _P, _F, _P, _P], _I),
     "eelg_cgc_fwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_cgc_bwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_csr_spmm": ([_P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P], _I),
@@ -78,6 +80,12 @@ class LinWDesc(ctypes.Structure):
                 ("ins", LinWIns * LINW_MAXINS)]
 
 RADIAL_MAXH = 3
+GATE_MAXBLK = 8
+
+
+class GateDesc(ctypes.Structure):
+    _fields_ = [("n_scal", _I), ("n_gates", _I), ("n_blk", _I), ("pad", _I),
+                ("blk_mul", _I * GATE_MAXBLK), ("blk_dim", _I * GATE_MAXBLK)]
 
 
 class RadialDesc(ctypes.Structure):

@@ -24,6 +24,8 @@ from .irreps import Irreps
 # grad-W launch shape: target workgroups and a cap on the node slices (partials)
 LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
 LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "1000000"))
+# the readout Gate as fused HIP passes (1) or torch elementwise ops (0)
+GATE_FUSED = os.environ.get("EELG_GATE_FUSED", "1") != "0"
 
 
 def _accept_output_mask(state_dict, key: str, irreps_out, covered, error_msgs) -> None:
@@ -275,6 +277,31 @@ class Linear(torch.nn.Module):
         return _IrrepsLinearFn.apply(_f32(x), weight, bias, self, side, residual, grad_mailbox)
 
 
+class _GateFn(torch.autograd.Function):
+    """e3nn ``nn.Gate`` as two fused HIP passes (``eelg_gate_fwd`` / ``eelg_gate_bwd``)."""
+
+    @staticmethod
+    def forward(ctx, x, gate: "Gate"):
+        from . import _lib
+        y = torch.empty(x.shape[0], gate.irreps_out.dim, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().eelg_gate_fwd(_lib.ptr(x), x.shape[0], ctypes.byref(gate._desc()),
+                                             float(gate.cst), _lib.ptr(y), _lib.stream(y)), "gate_fwd")
+        ctx.save_for_backward(x)
+        ctx.gate = gate
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _lib
+        (x,) = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        _lib.check(_lib.load().eelg_gate_bwd(_lib.ptr(x), _lib.ptr(gy), x.shape[0],
+                                             ctypes.byref(ctx.gate._desc()), float(ctx.gate.cst),
+                                             _lib.ptr(gx), _lib.stream(gx)), "gate_bwd")
+        return gx, None
+
+
 class Gate(torch.nn.Module):
     def __init__(self, irreps_scalars, irreps_gates, irreps_gated):
         super().__init__()
@@ -294,7 +321,22 @@ class Gate(torch.nn.Module):
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
+    def _desc(self):
+        from . import _lib
+        if getattr(self, "_gdesc", None) is None:
+            d = _lib.GateDesc()
+            d.n_scal, d.n_gates, d.n_blk = self.irreps_scalars.dim, self.irreps_gates.dim, len(self.irreps_gated)
+            if d.n_blk > _lib.GATE_MAXBLK:
+                raise NotImplementedError(f"gate: more than {_lib.GATE_MAXBLK} gated blocks")
+            for b, (mul, ir) in enumerate(self.irreps_gated):
+                d.blk_mul[b], d.blk_dim[b] = mul, ir.dim
+            self._gdesc = d
+        return self._gdesc
+
     def forward(self, x):
+        if x.is_cuda and x.dtype == torch.float32 and GATE_FUSED:
+            from .ops import _f32
+            return _GateFn.apply(_f32(x), self)
         # one torch.split instead of per-block slices: its backward is a single cat, where
         # slice backwards would each zero-fill a full [n, dim_in] gradient and add it up
         # (six zero-fill + add pairs per gate; the values are identical either way)

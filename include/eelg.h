@@ -98,6 +98,19 @@ int eelg_segment_sum_csr_bf16(const void* src, const int* rowptr, const int* idx
  * out[r, :] = scale * row_scale[r] * sum_pieces.  Same result contract as
  * eelg_segment_sum_csr (gnn/model.py:100-106 global mean pool), without the
  * one-wave-per-segment serialisation. */
+/* Gate nonlinearity of the readout (e3nn nn.Gate, gnn/blocks.py:268-273): rows
+ * x = [scalars | gates | gated blocks], y = [cst*silu(scalars) | gated block b channel u
+ * times cst*silu(gate of (b, u))], cst = normalize2mom(silu).  blk_mul / blk_dim: the gated
+ * blocks (mul copies of a (2l+1)-dim irrep, in row order); n_gates = sum of blk_mul.
+ * eelg_gate_bwd writes grad_x for grad_y (one fused pass instead of the split / mul / cat and
+ * their backward in torch). */
+#define EELG_GATE_MAXBLK 8
+typedef struct { int n_scal, n_gates, n_blk, pad; int blk_mul[EELG_GATE_MAXBLK]; int blk_dim[EELG_GATE_MAXBLK]; } eelg_gate_desc;
+int eelg_gate_fwd(const float* x, int n_nodes, const eelg_gate_desc* desc, float cst, float* y,
+                  void* stream);
+int eelg_gate_bwd(const float* x, const float* grad_y, int n_nodes, const eelg_gate_desc* desc,
+                  float cst, float* grad_x, void* stream);
+
 int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
                            const float* row_scale, float scale, int n_rows, int width, int n_split,
                            float* work, float* out, void* stream);

@@ -411,3 +411,31 @@ def test_linear_residual_epilogue(irreps):
     (y2 * g).sum().backward()
     assert torch.allclose(y1, y2, atol=1e-6, rtol=1e-6)
     assert torch.equal(gx1, x.grad) and torch.equal(gr1, r.grad) and torch.equal(gw1, lin.weight.grad)
+
+
+@pytest.mark.parametrize("scal,gates,gated", [
+    ("32x0e", "128x0e", "32x1o+32x2e+32x3o+32x4e"),     # the readout gate of the bench model
+    ("16x0e", "24x0e", "8x1o+16x2e"),
+    ("5x0e", "0x0e", ""),                               # scalars only
+])
+def test_gate_fused_matches_oracle(scal, gates, gated):
+    """eelg_gate_fwd / eelg_gate_bwd (the readout Gate, gnn/blocks.py:268-273) against the
+    oracle's fp64 Gate: value and grad-x, rel-to-max <= 1e-6 (fp32 silu)."""
+    from gnn.o3 import Gate
+    torch.manual_seed(11)
+    g = Gate(scal, gates if gates != "0x0e" else "", gated)
+    og = oo3.Gate(scal, gates if gates != "0x0e" else "", gated)
+    n = 517
+    x = torch.randn(n, g.irreps_in.dim, device=DEV, requires_grad=True)
+    gy = torch.randn(n, g.irreps_out.dim, device=DEV)
+    y = g(x)
+    (y * gy).sum().backward()
+    xo = x.detach().double().cpu().requires_grad_(True)
+    yo = og(xo)
+    (yo * gy.double().cpu()).sum().backward()
+
+    def rel(a, b):
+        return float((a.detach().double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30))
+    ey, ex = rel(y, yo.detach()), rel(x.grad, xo.grad)
+    record_parity(f"gate[{scal}|{gates}|{gated}]", fwd=ey, grad_x=ex, tol=1e-6)
+    assert ey < 1e-6 and ex < 1e-6, (ey, ex)
