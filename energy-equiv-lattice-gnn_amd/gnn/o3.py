@@ -23,7 +23,7 @@ from .irreps import Irreps
 
 # grad-W launch shape: target workgroups and a cap on the node slices (partials)
 LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
-LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "1000000"))
+LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "64"))
 # the readout Gate as fused HIP passes (1) or torch elementwise ops (0)
 GATE_FUSED = os.environ.get("EELG_GATE_FUSED", "1") != "0"
 
