@@ -132,35 +132,40 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
 // of a row, rows split over the grid; the gated block of an element is found by a walk over
 // the <= EELG_GATE_MAXBLK block offsets
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float gate_silu(float v) { return v / (1.0f + __expf(-v)); }
+__device__ __forceinline__ float gate_sig(float v) { return __frcp_rn(1.0f + __expf(-v)); }
+__device__ __forceinline__ float gate_silu(float v) { return v * gate_sig(v); }
 __device__ __forceinline__ float gate_dsilu(float v) {
-  const float s = 1.0f / (1.0f + __expf(-v));
+  const float s = gate_sig(v);
   return s * (1.0f + v * (1.0f - s));
 }
-// element jj of the concatenated gated blocks -> (gate index within the gates, first element
-// of its (block, channel) run, run length d)
-__device__ __forceinline__ void gate_locate(const eelg_gate_desc& g, int jj, int& gi, int& r0, int& d) {
+#define EELG_GATE_ROWBUF EELG_GATE_MAXGATED
+#define GATE_ROWS 4               // rows per workgroup (the lookup tables are built once per workgroup)
+
+// per-workgroup lookup tables: gated element -> its gate; gate -> first element of its run, d
+__device__ __forceinline__ void gate_tables(const eelg_gate_desc& g, unsigned short* tab,
+                                            unsigned short* r0s, unsigned char* ds) {
   int off = 0, goff = 0;
   for (int b = 0; b < g.n_blk; ++b) {
-    const int len = g.blk_mul[b] * g.blk_dim[b];
-    if (jj < off + len || b + 1 == g.n_blk) {
-      d = g.blk_dim[b];
-      const int u = (jj - off) / d;
-      gi = goff + u;
-      r0 = off + u * d;
-      return;
+    const int mul = g.blk_mul[b], d = g.blk_dim[b];
+    for (int e = threadIdx.x; e < mul * d; e += 256) tab[off + e] = (unsigned short)(goff + e / d);
+    for (int u = threadIdx.x; u < mul; u += 256) {
+      r0s[goff + u] = (unsigned short)(off + u * d);
+      ds[goff + u] = (unsigned char)d;
     }
-    off += len;
-    goff += g.blk_mul[b];
+    off += mul * d;
+    goff += mul;
   }
-  gi = r0 = 0;
-  d = 1;
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void gate_fwd_kernel(const float* __restrict__ x, int n_nodes,
                                                        eelg_gate_desc g, int din, int dout,
                                                        float cst, float* __restrict__ y) {
-  for (int n = blockIdx.x; n < n_nodes; n += gridDim.x) {
+  __shared__ unsigned short tab[EELG_GATE_MAXGATED], r0s[EELG_GATE_MAXGATES];
+  __shared__ unsigned char ds[EELG_GATE_MAXGATES];
+  gate_tables(g, tab, r0s, ds);
+  const int n1 = min(n_nodes, (int)(blockIdx.x + 1) * GATE_ROWS);
+  for (int n = blockIdx.x * GATE_ROWS; n < n1; ++n) {
     const float* __restrict__ xr = x + (size_t)n * din;
     float* __restrict__ yr = y + (size_t)n * dout;
     for (int j = threadIdx.x; j < dout; j += 256) {
@@ -168,9 +173,7 @@ __global__ __launch_bounds__(256) void gate_fwd_kernel(const float* __restrict__
         yr[j] = cst * gate_silu(xr[j]);
       } else {
         const int jj = j - g.n_scal;
-        int gi, r0, d;
-        gate_locate(g, jj, gi, r0, d);
-        yr[j] = xr[g.n_scal + g.n_gates + jj] * (cst * gate_silu(xr[g.n_scal + gi]));
+        yr[j] = xr[g.n_scal + g.n_gates + jj] * (cst * gate_silu(xr[g.n_scal + tab[jj]]));
       }
     }
   }
@@ -180,31 +183,32 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const float* __restrict__
                                                        const float* __restrict__ gy, int n_nodes,
                                                        eelg_gate_desc g, int din, int dout,
                                                        float cst, float* __restrict__ gx) {
-  for (int n = blockIdx.x; n < n_nodes; n += gridDim.x) {
+  __shared__ unsigned short tab[EELG_GATE_MAXGATED], r0s[EELG_GATE_MAXGATES];
+  __shared__ unsigned char ds[EELG_GATE_MAXGATES];
+  __shared__ float prod[EELG_GATE_ROWBUF];   // grad_y * x of the gated elements of one row
+  gate_tables(g, tab, r0s, ds);
+  const int gated0 = g.n_scal + g.n_gates, glen = dout - g.n_scal;
+  const int n1 = min(n_nodes, (int)(blockIdx.x + 1) * GATE_ROWS);
+  for (int n = blockIdx.x * GATE_ROWS; n < n1; ++n) {
     const float* __restrict__ xr = x + (size_t)n * din;
     const float* __restrict__ gr = gy + (size_t)n * dout;
     float* __restrict__ o = gx + (size_t)n * din;
-    const int gated0 = g.n_scal + g.n_gates;
-    for (int i = threadIdx.x; i < din; i += 256) {
-      const float v = xr[i];
-      if (i < g.n_scal) {
-        o[i] = gr[i] * cst * gate_dsilu(v);
-      } else if (i < gated0) {
-        // gate of (block b, channel u): sum over the run it scales of grad_y * x
-        const int gi = i - g.n_scal;
-        int off = 0, goff = 0, b = 0;
-        while (b + 1 < g.n_blk && gi >= goff + g.blk_mul[b]) { off += g.blk_mul[b] * g.blk_dim[b]; goff += g.blk_mul[b]; ++b; }
-        const int d = g.blk_dim[b], r0 = off + (gi - goff) * d;
-        float s = 0.0f;
-        for (int m = 0; m < d; ++m) s = fmaf(gr[g.n_scal + r0 + m], xr[gated0 + r0 + m], s);
-        o[i] = s * cst * gate_dsilu(v);
-      } else {
-        const int jj = i - gated0;
-        int gi, r0, d;
-        gate_locate(g, jj, gi, r0, d);
-        o[i] = gr[g.n_scal + jj] * (cst * gate_silu(xr[g.n_scal + gi]));
-      }
+    // pass 1 (coalesced): scalars, gated elements, and the products the gates sum
+    for (int i = threadIdx.x; i < g.n_scal; i += 256) o[i] = gr[i] * cst * gate_dsilu(xr[i]);
+    for (int jj = threadIdx.x; jj < glen; jj += 256) {
+      const float gyv = gr[g.n_scal + jj], xv = xr[gated0 + jj];
+      prod[jj] = gyv * xv;
+      o[gated0 + jj] = gyv * (cst * gate_silu(xr[g.n_scal + tab[jj]]));
     }
+    __syncthreads();
+    // pass 2: each gate sums its run of products from LDS
+    for (int gi = threadIdx.x; gi < g.n_gates; gi += 256) {
+      const int r0 = r0s[gi], d = ds[gi];
+      float s = 0.0f;
+      for (int m = 0; m < d; ++m) s += prod[r0 + m];
+      o[g.n_scal + gi] = s * cst * gate_dsilu(xr[g.n_scal + gi]);
+    }
+    __syncthreads();   // prod is rewritten by the next row
   }
 }
 
@@ -218,12 +222,15 @@ static int gate_check(const eelg_gate_desc* g, int* din, int* dout) {
     len += g->blk_mul[b] * g->blk_dim[b];
   }
   if (gates != g->n_gates) return fail(-2, "gate: %d gates for %d gated channels", g->n_gates, gates);
+  if (len > EELG_GATE_MAXGATED || gates > EELG_GATE_MAXGATES)
+    return fail(-2, "gate: %d gated elements / %d gates exceed the built tables (%d / %d)", len,
+                gates, EELG_GATE_MAXGATED, EELG_GATE_MAXGATES);
   *din = g->n_scal + g->n_gates + len;
   *dout = g->n_scal + len;
   return 0;
 }
 
-static int gate_grid(int n_nodes) { return n_nodes < 8192 ? n_nodes : 8192; }
+static int gate_grid(int n_nodes) { return (n_nodes + GATE_ROWS - 1) / GATE_ROWS; }
 
 // Few long segments (graph pooling: 32 graphs x 1024 nodes): split each segment into
 // n_split contiguous pieces, one wave per (segment, piece) -> work[seg][piece][:], then

@@ -81,6 +81,8 @@ class LinWDesc(ctypes.Structure):
 
 RADIAL_MAXH = 3
 GATE_MAXBLK = 8
+GATE_MAXGATED = 2048     # include/eelg.h EELG_GATE_MAXGATED / EELG_GATE_MAXGATES
+GATE_MAXGATES = 512
 
 
 class GateDesc(ctypes.Structure):

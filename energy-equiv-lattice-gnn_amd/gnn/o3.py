@@ -326,15 +326,20 @@ class Gate(torch.nn.Module):
         if getattr(self, "_gdesc", None) is None:
             d = _lib.GateDesc()
             d.n_scal, d.n_gates, d.n_blk = self.irreps_scalars.dim, self.irreps_gates.dim, len(self.irreps_gated)
-            if d.n_blk > _lib.GATE_MAXBLK:
-                raise NotImplementedError(f"gate: more than {_lib.GATE_MAXBLK} gated blocks")
             for b, (mul, ir) in enumerate(self.irreps_gated):
                 d.blk_mul[b], d.blk_dim[b] = mul, ir.dim
             self._gdesc = d
         return self._gdesc
 
+    def _fits_kernel(self) -> bool:
+        from . import _lib
+        return (len(self.irreps_gated) <= _lib.GATE_MAXBLK and self.irreps_gated.dim <= _lib.GATE_MAXGATED
+                and self.irreps_gates.dim <= _lib.GATE_MAXGATES)
+
     def forward(self, x):
-        if x.is_cuda and x.dtype == torch.float32 and GATE_FUSED:
+        # the fused HIP passes cover gates up to the kernels' table sizes; wider readouts use
+        # the torch form below (the readout tail is outside the HIP hot path)
+        if x.is_cuda and x.dtype == torch.float32 and GATE_FUSED and self._fits_kernel():
             from .ops import _f32
             return _GateFn.apply(_f32(x), self)
         # one torch.split instead of per-block slices: its backward is a single cat, where

@@ -105,6 +105,8 @@ int eelg_segment_sum_csr_bf16(const void* src, const int* rowptr, const int* idx
  * eelg_gate_bwd writes grad_x for grad_y (one fused pass instead of the split / mul / cat and
  * their backward in torch). */
 #define EELG_GATE_MAXBLK 8
+#define EELG_GATE_MAXGATED 2048   /* gated elements per row (the kernels' LDS lookup tables) */
+#define EELG_GATE_MAXGATES 512
 typedef struct { int n_scal, n_gates, n_blk, pad; int blk_mul[EELG_GATE_MAXBLK]; int blk_dim[EELG_GATE_MAXBLK]; } eelg_gate_desc;
 int eelg_gate_fwd(const float* x, int n_nodes, const eelg_gate_desc* desc, float cst, float* y,
                   void* stream);
