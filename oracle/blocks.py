@@ -27,6 +27,27 @@ def scatter_mean(src, index, dim_size):
     return s / cnt.view(-1, *([1] * (src.dim() - 1)))
 
 
+def scatter_reduce_order(src, index, n, reduce):
+    """torch_scatter ~2.0.9 ``scatter(reduce='max'|'min'|'mul')`` (the reference passes
+    ``global_reduction`` straight through, ``gnn/model.py:100-106``): rows that receive
+    nothing are 0 for max / min and 1 for mul.  Restated from torch_scatter's documented
+    semantics (the package is absent here: parity unpinned); a per-row loop, small cases only."""
+    rows = []
+    for g in range(n):
+        sel = src[index == g]
+        if sel.shape[0] == 0:
+            rows.append(torch.full((src.shape[1],), 1.0 if reduce == "mul" else 0.0, dtype=src.dtype))
+        elif reduce == "max":
+            rows.append(sel.max(0).values)
+        elif reduce == "min":
+            rows.append(sel.min(0).values)
+        elif reduce == "mul":
+            rows.append(sel.prod(0))
+        else:
+            raise ValueError(reduce)
+    return torch.stack(rows)
+
+
 class PositiveLayer(torch.nn.Module):
     """``gnn/blocks.py:185-229``."""
 

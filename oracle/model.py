@@ -10,7 +10,7 @@ import torch
 
 from . import o3
 from .blocks import (Cart_4_to_Mandel, GeneralNonLinearReadoutBlock, MACELayer, PositiveLayer,
-                     Spherical_to_Cartesian, scatter_mean, scatter_sum)
+                     Spherical_to_Cartesian, scatter_mean, scatter_reduce_order, scatter_sum)
 from .mace import get_edge_vectors_and_lengths
 
 
@@ -49,8 +49,10 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         out = self.nonlin_readout(node_ft)
         if self.global_reduction == "mean":
             g = scatter_mean(out, batch_idx, num_graphs)
-        elif self.global_reduction == "sum":
+        elif self.global_reduction in ("sum", "add"):
             g = scatter_sum(out, batch_idx, num_graphs)
+        elif self.global_reduction in ("max", "min", "mul"):
+            g = scatter_reduce_order(out, batch_idx, num_graphs, self.global_reduction)
         else:
             raise ValueError(self.global_reduction)
         stiff = self.sph_to_cart(self.linear(g))

@@ -439,3 +439,30 @@ def test_gate_fused_matches_oracle(scal, gates, gated):
     ey, ex = rel(y, yo.detach()), rel(x.grad, xo.grad)
     record_parity(f"gate[{scal}|{gates}|{gated}]", fwd=ey, grad_x=ex, tol=1e-6)
     assert ey < 1e-6 and ex < 1e-6, (ey, ex)
+
+
+@pytest.mark.parametrize("reduce", ["sum", "add", "max", "min", "mul"])
+def test_model_global_reductions_match_oracle(reduce):
+    """``global_reduction`` is any torch_scatter reduce (gnn/model.py:100-106); same
+    tolerances as the mean case above (1e-4 stiffness / loss, 1e-5 gradients)."""
+    from gnn.model import EnergyEquivGNN
+    from gnn.train import stiffness_loss
+    b, bd, csr, rmax = _setup()
+    p = params(2, max_edge_radius=rmax, global_reduction=reduce)
+    torch.manual_seed(0)
+    o = omodel.EnergyEquivGNN(p).double()
+    m = EnergyEquivGNN(p).to(DEV)
+    copy_params(o, m)
+    bo = batch_to(b, "cpu", torch.float64)
+    co = o(bo)["stiffness"]
+    lo = oracle_loss(co, bo.stiffness)
+    lo.backward()
+    cm = m(bd)["stiffness"]
+    lm = stiffness_loss(cm, bd.stiffness)
+    lm.backward()
+    po = dict(o.named_parameters())
+    worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
+    record_parity(f"model_reduce_{reduce}", stiffness=rel_err(cm, co), grad_params=worst)
+    assert rel_err(cm, co) < 1e-4
+    assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
+    assert worst < 1e-5

@@ -241,3 +241,24 @@ def test_storage_dtype_param_validation():
     assert storage_dtype(params(2, storage_dtype="bfloat16")) == torch.bfloat16
     with pytest.raises(ValueError):
         storage_dtype(params(2, storage_dtype="fp8"))
+
+
+@pytest.mark.parametrize("reduce", ["max", "min", "mul"])
+def test_segment_pool_order_matches_oracle(reduce):
+    """ops.segment_pool_order (global_reduction max / min / mul, gnn/model.py:100-106) vs the
+    oracle's torch_scatter restatement, with an empty graph; values and gradients, fp64."""
+    from gnn import ops
+    from oracle.blocks import scatter_reduce_order
+    torch.manual_seed(3)
+    sizes = torch.tensor([3, 0, 5, 1])
+    idx = torch.repeat_interleave(torch.arange(4), sizes)
+    src = torch.rand(int(sizes.sum()), 21, dtype=torch.float64) + 0.5
+    a = src.clone().requires_grad_(True)
+    b = src.clone().requires_grad_(True)
+    out = ops.segment_pool_order(a, sizes, reduce)
+    ref = scatter_reduce_order(b, idx, 4, reduce)
+    g = torch.randn_like(ref)
+    (out * g).sum().backward()
+    (ref * g).sum().backward()
+    assert torch.allclose(out, ref, rtol=1e-12, atol=0)
+    assert torch.allclose(a.grad, b.grad, rtol=1e-12, atol=1e-15)
