@@ -427,6 +427,34 @@ int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   return check_launch("tp_bwd_bf16");
 }
 
+// one half-wave per sender node, nbgroups input blocks on blockIdx.y
+int eelg_tp_bwd_sender(int cfg, const float* x, const float* sh, const float* w, const int* sperm,
+                       const int* srowptr, const int* receiver, int n_nodes,
+                       const float* grad_agg, float inv_norm, float* grad_w, float* grad_x,
+                       void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->bws, dim3((n_nodes + 7) / 8, c->nbgroups), dim3(256), 0,
+                     (hipStream_t)stream, x, sh, w, sperm, srowptr, receiver, n_nodes, grad_agg,
+                     inv_norm, grad_w, grad_x);
+  return check_launch("tp_bwd_sender");
+}
+
+int eelg_tp_bwd_sender_bf16(int cfg, const float* x, const float* sh, const void* w,
+                            const int* sperm, const int* srowptr, const int* receiver,
+                            int n_nodes, const float* grad_agg, float inv_norm, void* grad_w,
+                            float* grad_x, void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->bws_bf, dim3((n_nodes + 7) / 8, c->nbgroups), dim3(256), 0,
+                     (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sperm,
+                     srowptr, receiver, n_nodes, grad_agg, inv_norm,
+                     static_cast<unsigned short*>(grad_w), grad_x);
+  return check_launch("tp_bwd_sender_bf16");
+}
+
 int eelg_segment_sum_csr(const float* src, const int* rowptr, const int* idx,
                          const float* row_scale, float scale, int n_rows, int width, float* out,
                          void* stream) {

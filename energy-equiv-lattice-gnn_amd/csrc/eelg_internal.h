@@ -13,6 +13,13 @@ typedef void (*eelg_tp_fwd_bf_fn)(const float*, const float*, const unsigned sho
 typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned short*, const int*,
                                   const int*, int, const float*, float, unsigned short*,
                                   unsigned short*);
+// sender-order backward: (x, sh, w, sperm, srowptr, receiver, n_nodes, grad_agg, inv_norm,
+// grad_w, grad_x)
+typedef void (*eelg_tp_bws_fn)(const float*, const float*, const float*, const int*, const int*,
+                               const int*, int, const float*, float, float*, float*);
+typedef void (*eelg_tp_bws_bf_fn)(const float*, const float*, const unsigned short*, const int*,
+                                  const int*, const int*, int, const float*, float,
+                                  unsigned short*, float*);
 typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*, float*,
                                 float*);
@@ -29,6 +36,8 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_fn bwd;
   eelg_tp_fwd_bf_fn fwd_bf;
   eelg_tp_bwd_bf_fn bwd_bf;
+  eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
+  eelg_tp_bws_bf_fn bws_bf;
 };
 
 struct eelg_sc_cfg {

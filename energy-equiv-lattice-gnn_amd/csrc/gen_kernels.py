@@ -630,6 +630,94 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  default: break;")
     L.append("  }")
     L.append("}")
+
+    # ---------------- backward in sender order ----------------
+    # One half-wave owns one SENDER node and walks its out-edges through the sender CSR
+    # (srowptr / sperm): x[sender] is loaded once, grad_x is summed in registers and stored
+    # once per node, so the per-edge gxe [E, din] round trip and the segment sum that read
+    # it back disappear.  grad_w is written at each edge's own row as before.  Summation
+    # order over a sender's edges is the sperm order, the same as segment_sum_csr's.
+    L.append(f"__global__ __launch_bounds__(256) void tp_bws_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+    L.append("    const int* __restrict__ sperm, const int* __restrict__ srowptr,")
+    L.append("    const int* __restrict__ receiver, int n_nodes,")
+    L.append("    const float* __restrict__ gagg, float inv_norm,")
+    L.append(f"    {WT}* __restrict__ gw, float* __restrict__ gx) {{")
+    L.append("  const int lane = threadIdx.x & 63;")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append("  const int n = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
+    L.append("  if (n >= n_nodes) return;")
+    L.append("  const int p0 = srowptr[n], p1 = srowptr[n + 1];")
+    L.append("  switch (blockIdx.y) {")
+    for gi, grp in enumerate(bgroups):
+        l = grp[0].l1
+        d = 2 * l + 1
+        l2s = sorted({p.l2 for p in grp})
+        xs_ = [f"x{l}_{i}" for i in range(d)]
+        ys_ = [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)]
+        gxs = [f"gx{l}_{i}" for i in range(d)]
+        L.append(f"  case {gi}: {{ // input block l1 = {l}")
+        L.append("    float " + ", ".join(xs_) + ";")
+        L.append(f"    {{ const float* __restrict__ xs = x + (size_t)n * {din};")
+        L += ["      " + ln for ln in vec_load(xs_, "xs", f"{node_off[l]} + u * {d}")]
+        L.append("    }")
+        L.append("    float " + ", ".join(f"{v} = 0.0f" for v in gxs) + ";")
+        L.append("    int en = p0 < p1 ? sperm[p0] : 0;")
+        L.append("    for (int p = p0; p < p1; ++p) {")
+        L.append("      const int e = en;")
+        L.append("      en = p + 1 < p1 ? sperm[p + 1] : 0;")
+        L.append("      const int r = receiver[e];")
+        L.append(f"      const float* __restrict__ ye = sh + (size_t)e * {nshp};")
+        L.append(f"      const float* __restrict__ ge = gagg + (size_t)r * {dmid};")
+        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
+        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
+        L.append("      float " + ", ".join(ys_) + ";")
+        L += ["      " + ln for ln in sh_load(l2s, "", "ye")]
+
+        def pload(p):
+            d3 = 2 * p.l3 + 1
+            out = ["      float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
+            out += ["      " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
+                                                    f"{p.out_off} + u * {d3}")]
+            out.append(f"      float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
+            return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
+        code, _ = pload(grp[0])
+        L += code
+        for pi, p in enumerate(grp):
+            d3 = 2 * p.l3 + 1
+            d1 = 2 * p.l1 + 1
+            nxt_regs = []
+            if pi + 1 < len(grp):            # next path's loads in flight during this one
+                code, nxt_regs = pload(grp[pi + 1])
+                L += code
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
+            byik: Dict[Tuple[int, int], List[str]] = {}
+            for (i, j, k), c in _path_cg(p):
+                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
+            for (i, k), ts in byik.items():
+                L.append(f"        const float m{i}_{k} = {' + '.join(ts)};")
+            gterms = []
+            for k in range(d3):
+                ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
+                if ts:
+                    gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
+            gexpr = " + ".join(gterms) if gterms else "0.0f"
+            L.append(f"        gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
+            L.append(f"        const float hw = cp * w{p.slot};")
+            for i in range(d1):
+                ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
+                if ts:
+                    L.append(f"        gx{p.l1}_{i} = fmaf(hw, {' + '.join(ts)}, gx{p.l1}_{i});")
+            L.append("      }")
+            L.append("      " + pin(xs_ + gxs + ys_ + nxt_regs))
+        L.append("    }")
+        L.append(f"    float* __restrict__ gxo = gx + (size_t)n * {din};")
+        L += ["    " + ln for ln in vec_store(gxs, "gxo", f"{node_off[l]} + u * {d}")]
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
                 npaths=len(paths), nph=2 * TP_NPH if pk2 else TP_NPH, beph=TP_BWD_EPH,
                 sig=fnv1a64(tp_signature(node, sh, target)))
@@ -1274,7 +1362,7 @@ def main(outdir: str) -> None:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                      f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw}},')
+                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:

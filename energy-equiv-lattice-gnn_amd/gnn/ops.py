@@ -55,6 +55,10 @@ OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
 SC_CMAJOR_ON_SIDE = os.environ.get("EELG_SC_CMAJOR_SIDE", "0") != "0"   # measured equal; fused keeps fewer bytes
 # the contraction's coefficient gradient on the coefficient side stream (1) or in line (0)
 SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
+# TP backward in sender order (eelg_tp_bwd_sender) instead of per-edge gxe + sender segment sum.
+# Off: measured slower (r02s1: tp_bws 1.40 ms vs tp_bwd 1.05 + sender sum 0.16 ms; 1832 vs
+# 1862 graphs/s) -- each edge gathers its receiver's 29 KB grad_agg row out of receiver order.
+TP_BWD_SENDER = os.environ.get("EELG_TP_BWD_SENDER", "0") != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
@@ -217,11 +221,26 @@ def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
     cnt = (ptr[1:] - ptr[:-1]).to(torch.int64)
     if reduce == "mean":
         inv = 1.0 / cnt.clamp_min(1).to(torch.float32)
-    elif reduce == "sum":
+    elif reduce in ("sum", "add"):
         inv = torch.ones(num_graphs, device=src.device, dtype=torch.float32)
+    elif reduce in ("max", "min", "mul"):
+        return segment_pool_order(src, cnt, reduce)
     else:
-        raise ValueError(f"global_reduction {reduce!r} not supported")
+        raise ValueError(f"global_reduction {reduce!r} not supported "
+                         "(torch_scatter reduces: sum, add, mean, max, min, mul)")
     return _SegmentMean.apply(src, ptr, batch, inv)
+
+
+def segment_pool_order(src, cnt, reduce: str):
+    """torch_scatter ``scatter(..., reduce='max'|'min'|'mul')`` over sorted per-graph segments
+    of lengths ``cnt`` (``gnn/model.py:100-106`` passes any torch_scatter reduce).  Empty
+    graphs give 0 for max / min (torch_scatter fills untouched rows with 0) and 1 for mul
+    (its output starts at ones).  Readout tail, off the hot path: torch's segment_reduce
+    (one kernel, with autograd) on the pooled [N, 21] rows."""
+    if reduce == "mul":
+        return torch.segment_reduce(src, "prod", lengths=cnt, axis=0, unsafe=True, initial=1.0)
+    out = torch.segment_reduce(src, reduce, lengths=cnt, axis=0, unsafe=True)
+    return torch.where((cnt > 0)[:, None], out, torch.zeros((), dtype=out.dtype, device=out.device))
 
 
 # ---------------------------------------------------------------------------
@@ -261,8 +280,19 @@ class _TPInteraction(torch.autograd.Function):
         g = _f32(g)
         e = csr.num_edges
         gw = torch.empty_like(w)                       # same storage type as w
-        gxe = torch.empty(e, info["din"], device=x.device, dtype=w.dtype)
         lib = _lib.load()
+        if TP_BWD_SENDER:
+            # sender-order pass: grad_x summed per sender in registers, no gxe round trip
+            gx = torch.empty(csr.num_nodes, info["din"], device=x.device, dtype=torch.float32)
+            bws = lib.eelg_tp_bwd_sender_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_sender
+            tok = TIMER.start(f"tp_bwd_sender[din={info['din']}]")
+            _lib.check(bws(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sperm),
+                           _lib.ptr(csr.srowptr), _lib.ptr(csr.receiver), csr.num_nodes,
+                           _lib.ptr(g), float(ctx.inv_norm), _lib.ptr(gw), _lib.ptr(gx),
+                           _lib.stream(gx)), "tp_bwd_sender")
+            TIMER.stop(tok)
+            return gx, None, gw, None, None, None, None
+        gxe = torch.empty(e, info["din"], device=x.device, dtype=w.dtype)
         bwd = lib.eelg_tp_bwd_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd
         tok = TIMER.start(f"tp_bwd[din={info['din']}]")
         _lib.check(bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),

@@ -79,6 +79,21 @@ int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
                      const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                      void* grad_w, void* gxe, void* stream);
 
+/* Backward of eelg_tp_fwd in sender order: one pass over the sender CSR (srowptr [N+1],
+ * sperm [E] = edge ids sorted by sender) that writes grad_w[E, weight_numel] at each edge's
+ * row and grad_x[N, din] summed per sender in registers -- eelg_tp_bwd + the sender
+ * eelg_segment_sum_csr in one launch, without the gxe [E, din] intermediate.  Same
+ * reference call sites (gnn/blocks.py:591-597, the autograd of conv_tp + scatter).
+ * _bf16: w / grad_w as bf16 bit patterns; grad_x is fp32 either way. */
+int eelg_tp_bwd_sender(int cfg, const float* x, const float* sh, const float* w, const int* sperm,
+                       const int* srowptr, const int* receiver, int n_nodes,
+                       const float* grad_agg, float inv_norm, float* grad_w, float* grad_x,
+                       void* stream);
+int eelg_tp_bwd_sender_bf16(int cfg, const float* x, const float* sh, const void* w,
+                            const int* sperm, const int* srowptr, const int* receiver,
+                            int n_nodes, const float* grad_agg, float inv_norm, void* grad_w,
+                            float* grad_x, void* stream);
+
 /* CSR segmented sum (deterministic, no atomics):
  * out[r, :] = scale * row_scale[r] * sum_{j in [rowptr[r], rowptr[r+1])} src[idx ? idx[j] : j, :].
  * Replaces torch_scatter.scatter(..., reduce='sum'|'mean') (gnn/blocks.py:595-597,

@@ -118,3 +118,48 @@ def test_model_bf16_storage_matches_oracle(lmax):
     record_parity(f"bf16_model_l{lmax}", stiffness=rel_err(cm, co),
                   grad_all=rel_err(gm, go), cos_min=cos_min)
 
+
+@pytest.mark.parametrize("lmax,layer0,bf", [(4, False, False), (4, True, False), (3, False, False),
+                                            (4, False, True), (3, False, True)])
+def test_tp_bwd_sender_order_matches_edge_order(lmax, layer0, bf):
+    """eelg_tp_bwd_sender (grad_x summed per sender in registers) vs eelg_tp_bwd + the sender
+    segment sum, on a graph whose first 7 nodes send nothing (their grad_x must be 0).
+    grad_w: the same per-edge expression (fma contraction may differ) -> 1e-6 fp32, one
+    bf16 ulp (2^-8) with bf16 storage; grad_x fp32: same order, fma vs add
+    -> 1e-6; bf16 storage: the edge path rounds each per-edge term to bf16 -> 1e-2."""
+    from gnn import _lib, cg, ops
+    from gnn.irreps import Irreps
+    b, rmax = batch(4, 50, 200, 1234)
+    keep = b.edge_index[0] >= 7                       # nodes 0..6 have no out-edges
+    ei = b.edge_index[:, keep]
+    bd = b.to(DEV)
+    csr = ops.EdgeCSR.build(ei.to(DEV), b.node_attrs.shape[0])
+    sh_ir = Irreps.spherical_harmonics(lmax)
+    node = Irreps("32x0e") if layer0 else Irreps(
+        "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+    target = (sh_ir * 32).sort()[0].simplify()
+    idx, info = _lib.tp_config_by_sig(cg.fnv1a64(cg.tp_signature(node, sh_ir, target)))
+    sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[keep.to(DEV)][csr.perm],
+                           bd.edge_attr[keep.to(DEV)][csr.perm].reshape(-1), lmax, 6, 0.6, rmax)
+    torch.manual_seed(6)
+    n, e = csr.num_nodes, csr.num_edges
+    x = torch.randn(n, info["din"], device=DEV)
+    w = torch.randn(e, info["wn"], device=DEV)
+    w = w.to(torch.bfloat16) if bf else w
+    g = torch.randn(n, info["dmid"], device=DEV)
+    saved = ops.TP_BWD_SENDER
+    out = {}
+    try:
+        for flag in (True, False):
+            ops.TP_BWD_SENDER = flag
+            xx = x.clone().requires_grad_(True)
+            ww = w.clone().requires_grad_(True)
+            (ops.tp_interaction(xx, sh, ww, csr, idx, info, 0.25) * g).sum().backward()
+            out[flag] = (xx.grad, ww.grad)
+    finally:
+        ops.TP_BWD_SENDER = saved
+    (gxs, gws), (gxe, gwe) = out[True], out[False]
+    assert gxs.dtype == torch.float32 and gws.dtype == w.dtype
+    assert rel_err(gws, gwe) < (2 ** -8 if bf else 1e-6)
+    assert float(gxs[:7].abs().max()) == 0.0
+    assert rel_err(gxs, gxe) < (1e-2 if bf else 1e-6)
