@@ -55,10 +55,14 @@ OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
 SC_CMAJOR_ON_SIDE = os.environ.get("EELG_SC_CMAJOR_SIDE", "0") != "0"   # measured equal; fused keeps fewer bytes
 # the contraction's coefficient gradient on the coefficient side stream (1) or in line (0)
 SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
-# TP backward in sender order (eelg_tp_bwd_sender) instead of per-edge gxe + sender segment sum.
-# Off: measured slower (r02s1: tp_bws 1.40 ms vs tp_bwd 1.05 + sender sum 0.16 ms; 1832 vs
-# 1862 graphs/s) -- each edge gathers its receiver's 29 KB grad_agg row out of receiver order.
-TP_BWD_SENDER = os.environ.get("EELG_TP_BWD_SENDER", "0") != "0"
+# TP backward in sender order (eelg_tp_bwd_sender) instead of per-edge gxe + sender segment sum:
+# "1" always, "0" never, "auto" (default) for bf16 storage only.  fp32: measured slower (r02s1:
+# tp_bws 1.40 ms vs tp_bwd 1.05 + sender sum 0.16 ms; 1832 vs 1862 graphs/s) -- each edge
+# gathers its receiver's 29 KB grad_agg row out of receiver order.  bf16 storage (config 5):
+# equal speed (r02s2: 912.1 vs 912.4 graphs/s) and grad_x is summed in fp32 instead of from
+# per-edge terms rounded to bf16.
+_TBS = os.environ.get("EELG_TP_BWD_SENDER", "auto")
+TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
@@ -281,7 +285,8 @@ class _TPInteraction(torch.autograd.Function):
         e = csr.num_edges
         gw = torch.empty_like(w)                       # same storage type as w
         lib = _lib.load()
-        if TP_BWD_SENDER:
+        sender = TP_BWD_SENDER if TP_BWD_SENDER is not None else w.dtype == torch.bfloat16
+        if sender:
             # sender-order pass: grad_x summed per sender in registers, no gxe round trip
             gx = torch.empty(csr.num_nodes, info["din"], device=x.device, dtype=torch.float32)
             bws = lib.eelg_tp_bwd_sender_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_sender
