@@ -163,3 +163,33 @@ def test_tp_bwd_sender_order_matches_edge_order(lmax, layer0, bf):
     assert rel_err(gws, gwe) < (2 ** -8 if bf else 1e-6)
     assert float(gxs[:7].abs().max()) == 0.0
     assert rel_err(gxs, gxe) < (1e-2 if bf else 1e-6)
+
+
+@pytest.mark.parametrize("bf", [False, True])
+def test_torch_library_tp_interaction_matches_autograd_path(bf):
+    """torch.ops.eelg.tp_interaction (+ its registered autograd) vs ops.tp_interaction: the same
+    kernels in the same order -> bitwise; torch.library.opcheck on schema, fake tensor and
+    autograd registration."""
+    from gnn import _lib, ops, torch_ops  # noqa: F401
+    b, rmax = batch(4, 50, 200, 1234)
+    bd = b.to(DEV)
+    csr = ops.EdgeCSR.build(bd.edge_index, b.node_attrs.shape[0])
+    idx, info, _ = _lib.tp_config("tpB_l4")
+    sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[csr.perm],
+                           bd.edge_attr[csr.perm].reshape(-1), 4, 6, 0.6, rmax)
+    torch.manual_seed(7)
+    x = torch.randn(csr.num_nodes, info["din"], device=DEV)
+    w = torch.randn(csr.num_edges, info["wn"], device=DEV)
+    w = w.to(torch.bfloat16) if bf else w
+    g = torch.randn(csr.num_nodes, info["dmid"], device=DEV)
+    cargs = (csr.sender, csr.receiver, csr.rowptr, csr.sperm, csr.srowptr)
+    x1, w1 = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    a1 = torch.ops.eelg.tp_interaction(x1, sh, w1, *cargs, idx, 0.25)
+    (a1 * g).sum().backward()
+    x2, w2 = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    a2 = ops.tp_interaction(x2, sh, w2, csr, idx, info, 0.25)
+    (a2 * g).sum().backward()
+    assert torch.equal(a1, a2) and torch.equal(x1.grad, x2.grad) and torch.equal(w1.grad, w2.grad)
+    torch.library.opcheck(torch.ops.eelg.tp_interaction.default,
+                          (x.clone().requires_grad_(True), sh, w, *cargs, idx, 0.25),
+                          test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))

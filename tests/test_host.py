@@ -262,3 +262,25 @@ def test_segment_pool_order_matches_oracle(reduce):
     (ref * g).sum().backward()
     assert torch.allclose(out, ref, rtol=1e-12, atol=0)
     assert torch.allclose(a.grad, b.grad, rtol=1e-12, atol=1e-15)
+
+
+def test_torch_library_ops_fake_shapes():
+    """torch.ops.eelg.* (dispatcher-visible form of the fused interaction) propagate
+    shapes and dtypes on meta tensors without running HIP code."""
+    from gnn import _lib, torch_ops  # noqa: F401  (registers torch.ops.eelg)
+    idx, info, _ = _lib.tp_config("tpB_l4")
+    n, e = 10, 40
+
+    def meta(*s, dt=torch.float32):
+        return torch.empty(*s, device="meta", dtype=dt)
+    csr = [meta(e, dt=torch.int32), meta(e, dt=torch.int32), meta(n + 1, dt=torch.int32),
+           meta(e, dt=torch.int32), meta(n + 1, dt=torch.int32)]
+    out = torch.ops.eelg.tp_interaction(meta(n, info["din"]), meta(e, info["nsh"]),
+                                        meta(e, info["wn"]), *csr, idx, 0.25)
+    assert out.shape == (n, info["dmid"]) and out.dtype == torch.float32
+    gx, gw = torch.ops.eelg.tp_interaction_bwd(meta(n, info["dmid"]), meta(n, info["din"]),
+                                               meta(e, info["nsh"]),
+                                               meta(e, info["wn"], dt=torch.bfloat16), *csr, idx, 0.25)
+    assert gx.shape == (n, info["din"]) and gx.dtype == torch.float32
+    assert gw.shape == (e, info["wn"]) and gw.dtype == torch.bfloat16
+    assert torch.ops.eelg.segment_sum_csr(meta(e, 7), meta(n + 1, dt=torch.int32)).shape == (n, 7)
