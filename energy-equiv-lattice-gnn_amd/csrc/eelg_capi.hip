@@ -402,29 +402,44 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   return check_launch("tp_fwd_bf16");
 }
 
-int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
-                const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
-                float* grad_w, float* gxe, void* stream) {
+int eelg_tp_bwd_sorted(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                       const int* receiver, const int* spos, int n_edges, const float* grad_agg,
+                       float inv_norm, float* grad_w, float* gxe, void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_edges <= 0) return 0;
   hipLaunchKernelGGL(c->bwd, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, w, sender, receiver, n_edges, grad_agg, inv_norm,
-                     grad_w, gxe);
+                     grad_w, gxe, spos);
   return check_launch("tp_bwd");
 }
 
-int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
-                     const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
-                     void* grad_w, void* gxe, void* stream) {
+int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                float* grad_w, float* gxe, void* stream) {
+  return eelg_tp_bwd_sorted(cfg, x, sh, w, sender, receiver, nullptr, n_edges, grad_agg, inv_norm,
+                            grad_w, gxe, stream);
+}
+
+int eelg_tp_bwd_sorted_bf16(int cfg, const float* x, const float* sh, const void* w,
+                            const int* sender, const int* receiver, const int* spos, int n_edges,
+                            const float* grad_agg, float inv_norm, void* grad_w, void* gxe,
+                            void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_edges <= 0) return 0;
   hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sender,
                      receiver, n_edges, grad_agg, inv_norm, static_cast<unsigned short*>(grad_w),
-                     static_cast<unsigned short*>(gxe));
+                     static_cast<unsigned short*>(gxe), spos);
   return check_launch("tp_bwd_bf16");
+}
+
+int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
+                     const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
+                     void* grad_w, void* gxe, void* stream) {
+  return eelg_tp_bwd_sorted_bf16(cfg, x, sh, w, sender, receiver, nullptr, n_edges, grad_agg,
+                                 inv_norm, grad_w, gxe, stream);
 }
 
 // one half-wave per sender node, nbgroups input blocks on blockIdx.y

@@ -6,13 +6,13 @@
 typedef void (*eelg_tp_fwd_fn)(const float*, const float*, const float*, const int*, const int*, int,
                                float, float*);
 typedef void (*eelg_tp_bwd_fn)(const float*, const float*, const float*, const int*, const int*, int,
-                               const float*, float, float*, float*);
+                               const float*, float, float*, float*, const int*);
 // bf16 storage (bit patterns in unsigned short) of the edge-sized TP tensors
 typedef void (*eelg_tp_fwd_bf_fn)(const float*, const float*, const unsigned short*, const int*,
                                   const int*, int, float, float*);
 typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned short*, const int*,
                                   const int*, int, const float*, float, unsigned short*,
-                                  unsigned short*);
+                                  unsigned short*, const int*);
 // sender-order backward: (x, sh, w, sperm, srowptr, receiver, n_nodes, grad_agg, inv_norm,
 // grad_w, grad_x)
 typedef void (*eelg_tp_bws_fn)(const float*, const float*, const float*, const int*, const int*,

@@ -525,9 +525,11 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ receiver, int n_edges,")
     L.append("    const float* __restrict__ gagg, float inv_norm,")
-    L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe) {{")
+    L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe, const int* __restrict__ spos) {{")
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
+    # spos (optional): gxe row of edge e is spos[e], its position in sender order, so the sender
+    # sum reads gxe contiguously instead of gathering rows through sperm
     # a half-wave streams TP_BWD_EPH consecutive edges: while the last path of edge e
     # computes, edge e+1's x / SH rows and first path's grad_agg slice and weight are in
     # flight (its sender / receiver indices were loaded when edge e started)
@@ -571,7 +573,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
         L.append("      const float* __restrict__ ge = gagg + (size_t)rcur * " + str(dmid) + ";")
         L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
         L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
-        L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
+        L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)(spos ? spos[e] : e) * {din};")
         for i in range(d):
             L.append(f"      float gx{l}_{i} = 0.0f;")
         if EPH > 1:

@@ -32,6 +32,8 @@ _SIGS = {
     "eelg_tp_bwd": ([_I, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_tp_fwd_bf16": ([_I, _P, _P, _P, _P, _P, _I, _F, _P, _P], _I),
     "eelg_tp_bwd_bf16": ([_I, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
+    "eelg_tp_bwd_sorted": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
+    "eelg_tp_bwd_sorted_bf16": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_tp_bwd_sender": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_tp_bwd_sender_bf16": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_segment_sum_csr": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),

@@ -61,6 +61,11 @@ SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
 # gathers its receiver's 29 KB grad_agg row out of receiver order.  bf16 storage (config 5):
 # equal speed (r02s2: 912.1 vs 912.4 graphs/s) and grad_x is summed in fp32 instead of from
 # per-edge terms rounded to bf16.
+# edge-order backward: gxe rows stored at their sender-order position (eelg_tp_bwd_sorted), so
+# the sender sum reads them contiguously instead of gathering through sperm.  Bitwise-equal
+# results; measured equal (r02s3: sender sum 169 -> 137 us, tp_bwd 1036 -> 1128 us from the
+# scattered row stores; 1844 / 1855 vs 1844 / 1847 graphs/s), so off by default.
+TP_BWD_SPOS = os.environ.get("EELG_TP_BWD_SPOS", "0") != "0"
 _TBS = os.environ.get("EELG_TP_BWD_SENDER", "auto")
 TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
@@ -113,6 +118,16 @@ class EdgeCSR:
     @property
     def num_edges(self) -> int:
         return int(self.sender.shape[0])
+
+    def sender_pos(self) -> torch.Tensor:
+        """[E] int32 inverse of ``sperm``: the sender-order position of each edge (cached)."""
+        sp = getattr(self, "_spos", None)
+        if sp is None:
+            sp = torch.empty_like(self.sperm)
+            sp[self.sperm.long()] = torch.arange(self.sperm.shape[0], device=self.sperm.device,
+                                                 dtype=self.sperm.dtype)
+            self._spos = sp
+        return sp
 
     @staticmethod
     def from_dict(d: Dict, num_nodes: int) -> "EdgeCSR":
@@ -298,13 +313,15 @@ class _TPInteraction(torch.autograd.Function):
             TIMER.stop(tok)
             return gx, None, gw, None, None, None, None
         gxe = torch.empty(e, info["din"], device=x.device, dtype=w.dtype)
-        bwd = lib.eelg_tp_bwd_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd
+        spos = csr.sender_pos() if TP_BWD_SPOS else None
+        bwd = lib.eelg_tp_bwd_sorted_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_sorted
         tok = TIMER.start(f"tp_bwd[din={info['din']}]")
         _lib.check(bwd(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
-                       _lib.ptr(csr.receiver), e, _lib.ptr(g), float(ctx.inv_norm), _lib.ptr(gw),
-                       _lib.ptr(gxe), _lib.stream(gxe)), "tp_bwd")
+                       _lib.ptr(csr.receiver), _lib.ptr(spos), e, _lib.ptr(g), float(ctx.inv_norm),
+                       _lib.ptr(gw), _lib.ptr(gxe), _lib.stream(gxe)), "tp_bwd")
         TIMER.stop(tok)
-        gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
+        gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes,
+                             idx=None if spos is not None else csr.sperm)
         return gx, None, gw, None, None, None, None
 
 

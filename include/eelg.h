@@ -79,6 +79,18 @@ int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
                      const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                      void* grad_w, void* gxe, void* stream);
 
+/* eelg_tp_bwd / eelg_tp_bwd_bf16 with gxe written in sender order: the gxe row of edge e
+ * is spos[e] (spos = inverse of the sender-CSR permutation sperm), so the sender sum
+ * (eelg_segment_sum_csr with idx = NULL over srowptr) reads gxe contiguously.  Same
+ * reference call sites (gnn/blocks.py:591-597). */
+int eelg_tp_bwd_sorted(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                       const int* receiver, const int* spos, int n_edges, const float* grad_agg,
+                       float inv_norm, float* grad_w, float* gxe, void* stream);
+int eelg_tp_bwd_sorted_bf16(int cfg, const float* x, const float* sh, const void* w,
+                            const int* sender, const int* receiver, const int* spos, int n_edges,
+                            const float* grad_agg, float inv_norm, void* grad_w, void* gxe,
+                            void* stream);
+
 /* Backward of eelg_tp_fwd in sender order: one pass over the sender CSR (srowptr [N+1],
  * sperm [E] = edge ids sorted by sender) that writes grad_w[E, weight_numel] at each edge's
  * row and grad_x[N, din] summed per sender in registers -- eelg_tp_bwd + the sender

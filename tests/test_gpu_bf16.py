@@ -193,3 +193,34 @@ def test_torch_library_tp_interaction_matches_autograd_path(bf):
     torch.library.opcheck(torch.ops.eelg.tp_interaction.default,
                           (x.clone().requires_grad_(True), sh, w, *cargs, idx, 0.25),
                           test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+
+
+@pytest.mark.parametrize("bf", [False, True])
+def test_tp_bwd_sender_position_store_is_bitwise(bf):
+    """eelg_tp_bwd_sorted (gxe rows stored at their sender-order position, contiguous sender
+    sum) vs eelg_tp_bwd + the sperm-gathering sender sum: same values summed in the same order
+    -> bitwise equal grad_x and grad_w."""
+    from gnn import _lib, ops
+    b, rmax = batch(4, 50, 200, 1234)
+    bd = b.to(DEV)
+    csr = ops.EdgeCSR.build(bd.edge_index, b.node_attrs.shape[0])
+    idx, info, _ = _lib.tp_config("tpB_l4")
+    sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[csr.perm],
+                           bd.edge_attr[csr.perm].reshape(-1), 4, 6, 0.6, rmax)
+    torch.manual_seed(8)
+    x = torch.randn(csr.num_nodes, info["din"], device=DEV)
+    w = torch.randn(csr.num_edges, info["wn"], device=DEV)
+    w = w.to(torch.bfloat16) if bf else w
+    g = torch.randn(csr.num_nodes, info["dmid"], device=DEV)
+    saved = (ops.TP_BWD_SPOS, ops.TP_BWD_SENDER)
+    out = {}
+    try:
+        ops.TP_BWD_SENDER = False
+        for flag in (True, False):
+            ops.TP_BWD_SPOS = flag
+            xx, ww = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+            (ops.tp_interaction(xx, sh, ww, csr, idx, info, 0.25) * g).sum().backward()
+            out[flag] = (xx.grad, ww.grad)
+    finally:
+        ops.TP_BWD_SPOS, ops.TP_BWD_SENDER = saved
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
