@@ -59,22 +59,42 @@ def launch_ranks(n: int) -> None:
                        start_method="spawn")
 
 
-def init_dist():
-    """(world, rank, local_rank, device, n_devices) of this rank.  One process per GPU over
-    RCCL (backend 'nccl'); when there are fewer visible devices than ranks (a rehearsal on a
-    1-GPU box) the ranks share devices and talk over gloo instead."""
+def init_dist(rehearsal: bool = False):
+    """(world, rank, local_rank, device, n_devices, backend) of this rank.  One process per GPU
+    over RCCL (backend 'nccl').  With fewer visible devices than ranks the ranks would have to
+    share devices over gloo: that is only a rehearsal of the multi-rank code path, not a
+    multi-GPU measurement, so it is refused unless ``--rehearsal`` is given (and the JSON line
+    then names the backend and says so)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local_rank % max(ndev, 1))
-    torch.cuda.set_device(dev)
+    backend = None
     if world > 1:
         if ndev >= world:
-            dist.init_process_group("nccl", device_id=dev)
+            backend = "nccl"
+        elif rehearsal:
+            backend = "gloo"
         else:
-            dist.init_process_group("gloo")
-    return world, rank, local_rank, dev, min(world, ndev)
+            raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPU(s): refusing to report a "
+                             f"dp{world} number over gloo on shared devices (pass --rehearsal to run "
+                             "the multi-rank path anyway, labelled as a rehearsal)")
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    elif backend == "gloo":
+        dist.init_process_group("gloo")
+    return world, rank, local_rank, dev, min(world, ndev), backend
+
+
+def params_equal_across_ranks(params) -> bool:
+    """Bitwise equality of every parameter across ranks (elementwise max == min all-reduce)."""
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    hi, lo = flat.clone(), flat.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))
 
 
 def make_params(layers: int, max_edge_radius: float, lmax: int = 4, storage: str = "float32"):
@@ -235,7 +255,7 @@ def main_cgc(args):
     """BASELINE config 4: CGC / mCGC (scripts/train_cgcnn_*.py) on the same synthetic lattices.
     One step = forward + loss + backward + flat all-reduce + AdamW (hidden 128 / 64, 3 passes)."""
     from argparse import Namespace
-    world, rank, local_rank, dev, n_dev = init_dist()
+    world, rank, local_rank, dev, n_dev, backend = init_dist(args.rehearsal)
     from gnn import cgc, ops
     from gnn.data import collate
     from gnn.parallel import FlatGradAllReduce, broadcast_parameters
@@ -305,6 +325,7 @@ def main_cgc(args):
                "config": {"workload": f"{args.model} hidden {hid}, {args.batch} graphs/GPU x "
                                       f"{args.nodes} nodes/{args.edges} edges, fwd+loss+bwd+allreduce+AdamW",
                           "global_batch": args.batch * world, "parallelism": f"graph-sharded dp{world}"},
+               "backend": backend, "rehearsal": backend == "gloo",
                "loss": round(float(loss.item()), 6), "roofline": roof, "cpu_baseline": None}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_cgc(modified, p, args.nodes, args.edges, min(args.cpu_budget, 10.0))
@@ -336,6 +357,12 @@ def main():
                     help="AdamW implementation (same update rule)")
     ap.add_argument("--storage", default="float32", choices=["float32", "bfloat16"],
                     help="storage type of the edge-sized interaction tensors (fp32 arithmetic)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="N > 1 ranks on fewer GPUs (shared devices, gloo): exercises the multi-rank "
+                         "path; the line is labelled a rehearsal, not a multi-GPU measurement")
+    ap.add_argument("--check-params", action="store_true",
+                    help="N > 1: check after the timed steps that every rank holds bitwise-equal "
+                         "parameters (reported as params_equal_across_ranks)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="2 = BASELINE configs[1] (default); 5 = configs[4]: lmax 3, ~5k-node "
                          "lattices (5000 nodes / 20000 edges), bf16 storage, fp32 accumulate")
@@ -350,7 +377,7 @@ def main():
     if args.model != "egnn":
         return main_cgc(args)
 
-    world, rank, local_rank, dev, n_dev = init_dist()
+    world, rank, local_rank, dev, n_dev, backend = init_dist(args.rehearsal)
 
     from gnn import EnergyEquivGNN, ops
     from gnn.data import collate
@@ -407,6 +434,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ksum = ops.TIMER.summary()
+    same = params_equal_across_ranks(plist) if (world > 1 and args.check_params) else None
 
     if rank == 0:
         n_tot = args.batch * args.nodes
@@ -453,10 +481,13 @@ def main():
                        "global_batch": args.batch * world, "nodes_per_graph": args.nodes,
                        "edges_per_graph": args.edges, "layers": args.layers,
                        "parallelism": f"graph-sharded dp{world}"},
+            "backend": backend, "rehearsal": backend == "gloo",
             "loss": round(float(loss.item()), 6),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if same is not None:
+            out["params_equal_across_ranks"] = same
         if args.kernel_summary:
             print(json.dumps(ksum, indent=1), file=sys.stderr)
         print(json.dumps(out), flush=True)

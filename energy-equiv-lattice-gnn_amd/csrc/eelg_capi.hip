@@ -268,6 +268,67 @@ __global__ __launch_bounds__(256) void segment_combine_kernel(
   out[i] = acc * scale * (row_scale ? row_scale[row] : 1.0f);
 }
 
+// torch_scatter's order reductions over CSR segments (reduce = max / min / mul): one thread
+// per (row, column), columns fastest (coalesced rows).  max / min keep the FIRST extreme of
+// the segment (strict compare) and its position, so the backward routes the whole gradient
+// to that one element as torch_scatter's scatter_max / scatter_min do; rows with no entries
+// give 0 (max / min) or 1 (mul) and position -1.
+enum { SEG_MAX = 0, SEG_MIN = 1, SEG_MUL = 2 };
+
+__global__ __launch_bounds__(256) void segment_order_kernel(
+    const float* __restrict__ src, const int* __restrict__ rowptr, int n_rows, int width, int op,
+    float* __restrict__ out, int* __restrict__ arg) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)n_rows * width) return;
+  const int row = (int)(i / width), c = (int)(i - (long long)row * width);
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  if (op == SEG_MUL) {
+    float p = 1.0f;
+    for (int j = beg; j < end; ++j) p *= src[(size_t)j * width + c];
+    out[i] = p;
+    return;
+  }
+  float best = 0.0f;
+  int at = -1;
+  for (int j = beg; j < end; ++j) {
+    const float v = src[(size_t)j * width + c];
+    if (at < 0 || (op == SEG_MAX ? v > best : v < best)) { best = v; at = j; }
+  }
+  out[i] = best;
+  if (arg) arg[i] = at;
+}
+
+// backward: every source row of a segment gets its gradient (no zero-fill needed when the
+// segments cover the rows): max / min -> g at the kept position, 0 elsewhere; mul -> g times
+// the product of the segment's other entries (exact with zeros: counted, not divided by)
+__global__ __launch_bounds__(256) void segment_order_bwd_kernel(
+    const float* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ arg,
+    const float* __restrict__ g, int n_rows, int width, int op, float* __restrict__ gsrc) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)n_rows * width) return;
+  const int row = (int)(i / width), c = (int)(i - (long long)row * width);
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  const float gi = g[i];
+  if (op != SEG_MUL) {
+    const int at = arg[i];
+    for (int j = beg; j < end; ++j) gsrc[(size_t)j * width + c] = j == at ? gi : 0.0f;
+    return;
+  }
+  // product of the others = (product before j) * (product after j): a reverse pass leaves the
+  // suffix products in gsrc, a forward pass multiplies in the prefix (no division, so zeros
+  // are exact)
+  float s = 1.0f;
+  for (int j = end - 1; j >= beg; --j) {
+    gsrc[(size_t)j * width + c] = s;
+    s *= src[(size_t)j * width + c];
+  }
+  float p = 1.0f;
+  for (int j = beg; j < end; ++j) {
+    gsrc[(size_t)j * width + c] = gi * (p * gsrc[(size_t)j * width + c]);
+    p *= src[(size_t)j * width + c];
+  }
+}
+
 // Sparse (CSR) x dense with strided operands: out[r, c] = sum_j val[j] * B[col[j], c].
 // Four lanes per (r, c) (c fastest across lane quads) split a row's nonzeros and are
 // combined with two xor-shuffles in a fixed order, so long rows (U_sym^T: ~120 nnz) do
@@ -494,6 +555,28 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
   hipLaunchKernelGGL(segment_combine_kernel, dim3((n_rows * width + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, work, row_scale, scale, n_rows, width, n_split, out);
   return check_launch("segment_sum_split");
+}
+
+int eelg_segment_order(const float* src, const int* rowptr, int n_rows, int width, int op,
+                       float* out, int* arg, void* stream) {
+  if (op < SEG_MAX || op > SEG_MUL) return fail(-2, "segment_order: op %d (0 max, 1 min, 2 mul)", op);
+  if (op != SEG_MUL && !arg) return fail(-2, "segment_order: max / min need the position output");
+  if (n_rows <= 0 || width <= 0) return 0;
+  const long long n = (long long)n_rows * width;
+  hipLaunchKernelGGL(segment_order_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, src, rowptr, n_rows, width, op, out, arg);
+  return check_launch("segment_order");
+}
+
+int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, const float* grad_out,
+                           int n_rows, int width, int op, float* grad_src, void* stream) {
+  if (op < SEG_MAX || op > SEG_MUL) return fail(-2, "segment_order_bwd: op %d (0 max, 1 min, 2 mul)", op);
+  if (op != SEG_MUL && !arg) return fail(-2, "segment_order_bwd: max / min need the positions");
+  if (n_rows <= 0 || width <= 0) return 0;
+  const long long n = (long long)n_rows * width;
+  hipLaunchKernelGGL(segment_order_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, src, rowptr, arg, grad_out, n_rows, width, op, grad_src);
+  return check_launch("segment_order_bwd");
 }
 
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,

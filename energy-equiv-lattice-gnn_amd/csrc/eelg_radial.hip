@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
 // ---------------------------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------------------------
-static int radial_check(const eelg_radial_desc* d, int n_edges) {
+static int radial_check(const eelg_radial_desc* d, int n_edges, int out_es) {
   if (!d) return eelg_fail(-2, "radial: null descriptor");
   if (d->hidden != 32 && d->hidden != 64)
     return eelg_fail(-2, "radial: hidden width %d not built (32 or 64)", d->hidden);
@@ -543,7 +543,8 @@ static int radial_check(const eelg_radial_desc* d, int n_edges) {
   if (n_edges < 0) return eelg_fail(-2, "radial: negative edge count");
   // buffer descriptors address each stream with 32-bit byte offsets (< 2 GiB)
   const long long e = n_edges;
-  if (e * d->n_out * 4 >= (1LL << 31) || e * d->hidden * d->n_hidden * 4 >= (1LL << 31))
+  // (out_es: bytes per output element, 4 fp32 / 2 bf16; the host splits larger edge sets)
+  if (e * d->n_out * out_es >= (1LL << 31) || e * d->hidden * d->n_hidden * 4 >= (1LL << 31))
     return eelg_fail(-2, "radial: %d edges x %d outputs exceed the 2 GiB per-stream limit; "
                          "split the edge set", n_edges, d->n_out);
   return 0;
@@ -603,7 +604,7 @@ int eelg_radial_plan(int n_edges, int n_out, int* n_part, int* n_split) {
 
 int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const float* wo_t,
                     int out_bf16, float* zsave, void* out, void* stream) {
-  if (int rc = radial_check(d, n_edges)) return rc;
+  if (int rc = radial_check(d, n_edges, out_bf16 ? 2 : 4)) return rc;
   if (n_edges == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool bf = out_bf16 != 0;
@@ -615,7 +616,7 @@ int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, 
 int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
                     const float* wo, const float* zsave, const float* feats, float* grad_h,
                     float* part_h, float* part_wo, void* stream) {
-  if (int rc = radial_check(d, n_edges)) return rc;
+  if (int rc = radial_check(d, n_edges, grad_bf16 ? 2 : 4)) return rc;
   if (n_edges == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool bf = grad_bf16 != 0;

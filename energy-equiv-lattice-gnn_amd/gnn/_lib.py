@@ -39,6 +39,8 @@ _SIGS = {
     "eelg_segment_sum_csr": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_csr_bf16": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_split": ([_P, _P, _P, _P, _F, _I, _I, _I, _P, _P, _P], _I),
+    "eelg_segment_order": ([_P, _P, _I, _I, _I, _P, _P, _P], _I),
+    "eelg_segment_order_bwd": ([_P, _P, _P, _P, _I, _I, _I, _P, _P], _I),
     "eelg_gate_fwd": ([_P, _I, _P, _F, _P, _P], _I),
     "eelg_gate_bwd": ([_P, _P, _I, _P, _F, _P, _P], _I),
     "eelg_cgc_fwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),

@@ -23,13 +23,18 @@ import torch
 
 from . import _lib, cg, kernel_sets, ops
 from .irreps import Irreps
-from .mace import SymmetricContraction
+from .mace import SymmetricContraction, reshape_irreps
 from .o3 import Gate, GradMailbox, Linear, TensorProduct
 
 # the layer residual's gradient summed in linear_up's grad-x epilogue (1) or by autograd (0)
 RESIDUAL_GRAD_FUSED = os.environ.get("EELG_RESIDUAL_GRAD_FUSED", "1") != "0"
 
 EdgeIndex = Union[torch.Tensor, ops.EdgeCSR]
+
+# torch_scatter reduces accepted for interaction_reduction (gnn/blocks.py:595-597): 'sum' is
+# the fused kernel (the path scripts/train_main.py:32 uses); 'mean' scales its rows by the
+# clamped in-degree; max / min / mul reduce the per-edge messages (ops.per_edge_csr)
+REDUCTIONS = ("sum", "add", "mean", "max", "min", "mul")
 
 
 def as_csr(edge_index: EdgeIndex, num_nodes: int, *edge_tensors):
@@ -63,11 +68,23 @@ class PositiveLayer(torch.nn.Module):
         return self.func(c)
 
 
-class GeneralNonLinearReadoutBlock(torch.nn.Module):
-    """``gnn/blocks.py:250-283``."""
+def _is_silu(gate) -> bool:
+    return (gate is None or gate is torch.nn.functional.silu or isinstance(gate, torch.nn.SiLU)
+            or gate is torch.nn.SiLU)
 
-    def __init__(self, irreps_in, hidden_irreps, irreps_out, gate=None):
+
+class GeneralNonLinearReadoutBlock(torch.nn.Module):
+    """``gnn/blocks.py:250-283``.  ``gate`` is the activation of the scalars and the gates; the
+    reference model passes ``torch.nn.functional.silu`` (``gnn/model.py:78-83``), which the
+    fused Gate kernels implement (with e3nn's normalize2mom constant).  Any other activation
+    raises instead of being silently replaced by SiLU."""
+
+    def __init__(self, irreps_in, hidden_irreps, irreps_out, gate=torch.nn.functional.silu):
         super().__init__()
+        if not _is_silu(gate):
+            raise NotImplementedError(
+                f"GeneralNonLinearReadoutBlock(gate={gate!r}): the Gate kernels are built for "
+                "SiLU (torch.nn.functional.silu, as gnn/model.py:78-83 passes)")
         hidden_irreps, irreps_out = Irreps(hidden_irreps), Irreps(irreps_out)
         self.hidden_irreps, self.irreps_out = hidden_irreps, irreps_out
         scal = Irreps([(m, ir) for m, ir in hidden_irreps if ir.l == 0 and ir in irreps_out])
@@ -110,15 +127,23 @@ class Cart_4_to_Mandel(torch.nn.Module):  # noqa: N801
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
+        absent = []
         for name in ("mask", "rows", "cols"):
             t = state_dict.get(prefix + name)
             mine = getattr(self, name)
-            if t is not None and (t.shape != mine.shape or not torch.allclose(
-                    t.detach().cpu().double(), mine.cpu().double(), rtol=1e-6, atol=0)):
+            if t is None:
+                absent.append(prefix + name)
+            elif t.shape != mine.shape or not torch.allclose(
+                    t.detach().cpu().double(), mine.cpu().double(), rtol=1e-6, atol=0):
                 error_msgs.append(f"{prefix}{name}: differs from the reference's Cart_4_to_Mandel "
                                   "tables (gnn/blocks.py:395-417); refusing to load")
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
+        # derived tables: a checkpoint without them (written by this package before they were
+        # registered) keeps the derived values instead of failing a strict load
+        for k in absent:
+            if k in missing_keys:
+                missing_keys.remove(k)
 
     def forward(self, c):
         return (c.reshape(c.shape[0], 81) @ self.map).view(c.shape[0], 6, 6)
@@ -142,6 +167,7 @@ class EquivariantProductBlock(torch.nn.Module):
     def __init__(self, node_feats_irreps, target_irreps, correlation: int, use_sc: bool = True):
         super().__init__()
         node_feats_irreps = Irreps(node_feats_irreps)
+        self.reshape = reshape_irreps(node_feats_irreps)   # reference API; the path reads rows
         self.use_sc = use_sc
         mul = node_feats_irreps.count("0e")
         sc_out = Irreps([(mul, ir) for _, ir in Irreps(target_irreps)])
@@ -173,9 +199,10 @@ class TensorProductInteractionBlock(torch.nn.Module):
         self._irreps_out = Irreps(irreps_out)
         self.agg_norm_const = float(agg_norm_const)
         self.reduce = reduce.lower()
-        if self.reduce != "sum":
-            raise NotImplementedError("only interaction_reduction='sum' is on the hot path "
-                                      "(the PNA branch is out of scope, SURVEY.md section 2)")
+        if self.reduce not in REDUCTIONS:
+            raise NotImplementedError(
+                f"interaction_reduction {reduce!r}: the torch_scatter reduces {sorted(REDUCTIONS)} "
+                "are built ('pna' is out of scope, SURVEY.md section 2)")
         # fail at construction, with the supported list, for structures without generated kernels
         kernel_sets.check_tp(self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
         self.linear_up = Linear(self._node_feats_irreps, self._node_feats_irreps)
@@ -230,7 +257,15 @@ class TensorProductInteractionBlock(torch.nn.Module):
         idx, info = self._config()
         x = self.linear_up(node_feats, grad_mailbox=grad_mailbox)
         w = self.radial_weights(edge_feats) if tp_weights is None else tp_weights
-        agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, 1.0 / self.agg_norm_const)
+        inv = 1.0 / self.agg_norm_const
+        if self.reduce in ("sum", "add"):
+            agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv)
+        elif self.reduce == "mean":
+            agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv) * ops.in_degree_scale(csr)[:, None]
+        else:
+            # max / min / mul of the per-edge messages, then / agg_norm_const as the reference
+            m = ops.tp_interaction(x, edge_attrs, w, ops.per_edge_csr(csr), idx, info, 1.0)
+            agg = ops.segment_order(m, csr.rowptr, csr.num_nodes, self.reduce, covered=True) * inv
         return self.linear(agg), None
 
 

@@ -10,6 +10,8 @@ dense ``[N, 32, 2l+1, 25, 25]`` intermediate of the reference never exists.
 """
 from __future__ import annotations
 
+import functools
+
 import torch
 
 from . import _lib, cg, kernel_sets, ops
@@ -24,6 +26,47 @@ def get_edge_vectors_and_lengths(positions, edge_index, shifts):
     sender, receiver = edge_index
     vectors = positions[receiver] - positions[sender] + shifts
     return vectors, torch.linalg.norm(vectors, dim=-1, keepdim=True)
+
+
+class reshape_irreps(torch.nn.Module):  # noqa: N801
+    """``gnn/mace.py:316-332``: mul-major rows ``[N, Σ mul·d]`` -> ``[N, mul, Σ d]``.  The
+    product block keeps it as a submodule for API parity; its own path reads the rows."""
+
+    def __init__(self, irreps) -> None:
+        super().__init__()
+        self.irreps = Irreps(irreps)
+
+    def forward(self, tensor: torch.Tensor) -> torch.Tensor:
+        n = tensor.shape[0]
+        fields, ix = [], 0
+        for mul, ir in self.irreps:
+            d = ir.dim
+            fields.append(tensor[:, ix: ix + mul * d].reshape(n, mul, d))
+            ix += mul * d
+        return torch.cat(fields, dim=-1)
+
+
+def unreshape_irreps(irreps: Irreps, t: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``reshape_irreps``: ``[N, mul, Σ d]`` -> mul-major rows ``[N, Σ mul·d]``."""
+    n, mul = t.shape[0], t.shape[1]
+    rows, ix = [], 0
+    for m, ir in irreps:
+        if m != mul:
+            raise ValueError(f"reshape_irreps layout needs one multiplicity, got {irreps}")
+        rows.append(t[:, :, ix: ix + ir.dim].reshape(n, mul * ir.dim))
+        ix += ir.dim
+    if ix != t.shape[2]:
+        raise ValueError(f"input {tuple(t.shape)} does not match {irreps}")
+    return torch.cat(rows, dim=1).contiguous()
+
+
+@functools.lru_cache(maxsize=None)
+def _reference_U(coupling: str, l: int, nu: int) -> torch.Tensor:
+    """The reference's ``U_matrix_{nu}`` buffer (fp32, reference shape), built once per process
+    and shared by every layer's ``state_dict()`` (≈217 MB per lmax-4 layer): periodic
+    checkpointing does not rebuild it.  Like any state_dict entry it aliases held state."""
+    shape = cg.reference_U_shape(coupling, l, nu)
+    return torch.tensor(cg.U_matrix(coupling, l, nu), dtype=torch.float32).reshape(shape)
 
 
 class Contraction(torch.nn.Module):
@@ -82,10 +125,7 @@ class SymmetricContraction(torch.nn.Module):
         the device), so a checkpoint of this model loads strictly into the reference."""
         for l, nu, key in module._u_keys(prefix):
             u = module._u_loaded.get((l, nu))
-            if u is None:
-                shape = cg.reference_U_shape(module._coupling, l, nu)
-                u = torch.tensor(cg.U_matrix(module._coupling, l, nu), dtype=torch.float32).reshape(shape)
-            state_dict[key] = u
+            state_dict[key] = u if u is not None else _reference_U(module._coupling, l, nu)
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
@@ -94,7 +134,14 @@ class SymmetricContraction(torch.nn.Module):
         a different path order or sign convention) is adopted: its symmetrisation replaces
         the matching block of ``u_sym``, so the contraction computes exactly what the
         reference computes with that U and the loaded weights.  A U with symmetric weight on
-        monomials the generated kernels do not evaluate raises."""
+        monomials the generated kernels do not evaluate raises.
+
+        Every load starts from the derived basis: a block not carried by (or equal to the
+        derived one in) this checkpoint goes back to the derived block, so loading a standard
+        checkpoint after one in another basis computes with the derived U again.  The adopted
+        blocks are computed first and written only when every U of the module checked out."""
+        plan = None
+        adopted, loaded, failed = [], {}, False
         for l, nu, key in list(self._u_keys(prefix)):
             if key not in state_dict:
                 continue
@@ -103,21 +150,29 @@ class SymmetricContraction(torch.nn.Module):
             if tuple(u.shape) != want:
                 error_msgs.append(f"size mismatch for {key}: copying a param with shape "
                                   f"{tuple(u.shape)}, the reference shape is {want}")
+                failed = True
                 continue
             ref = torch.from_numpy(cg.U_matrix(self._coupling, l, nu)).reshape(want)
             if float((u - ref).abs().max()) <= 1e-6 * float(ref.abs().max()):
-                self._u_loaded.pop((l, nu), None)
                 continue
-            plan = cg.symcon_plan(self._coupling, self._ls, self.correlation)
+            plan = plan or cg.symcon_plan(self._coupling, self._ls, self.correlation)
             try:
                 k0, block = cg.symcon_block_from_U(plan, l, nu, u.numpy())
             except ValueError as e:
                 error_msgs.append(f"{key}: {e}")
+                failed = True
                 continue
+            adopted.append((k0, block))
+            loaded[(l, nu)] = u.to(torch.float32)
+        if not failed:
+            plan = plan or cg.symcon_plan(self._coupling, self._ls, self.correlation)
+            fresh = torch.tensor(plan.ubig, dtype=torch.float64)
+            for k0, block in adopted:
+                fresh[:, k0: k0 + block.shape[1]] = torch.from_numpy(block)
             with torch.no_grad():
-                self.u_sym[:, k0: k0 + block.shape[1]] = torch.from_numpy(block).to(self.u_sym)
+                self.u_sym.copy_(fresh.to(self.u_sym))
             self._u_csr = None
-            self._u_loaded[(l, nu)] = u.to(torch.float32)
+            self._u_loaded = loaded
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
@@ -141,7 +196,18 @@ class SymmetricContraction(torch.nn.Module):
             return ops.symcon_coefficients(self.weight_matrix(), self._u_csr)
         return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, y: torch.Tensor = None) -> torch.Tensor:
+        """``x``: the node rows ``[N, Σ mul·(2l+1)]`` in e3nn mul-major order (the fast path
+        used by ``EquivariantProductBlock``), or the reference's ``reshape_irreps`` output
+        ``[N, mul, Σ(2l+1)]`` (``gnn/mace.py:171-175,316-332``; that layout is converted back
+        to rows, one copy).  ``y`` is the reference's element attribute, unused in its
+        non-element-dependent branch (``gnn/mace.py:261-275``); it must be None here.
+        Returns ``[N, Σ mul·(2l_out+1)]`` mul-major, as the reference's ``torch.cat``."""
+        if y is not None:
+            raise NotImplementedError("element-dependent symmetric contraction (y given) is not "
+                                      "on the hot path: the model passes y=None (gnn/blocks.py:486)")
+        if x.dim() == 3:
+            x = unreshape_irreps(self.irreps_in, x)
         idx, info = self._config()
         side = ops.side_stream(x.device, 1) if (ops.OVERLAP and x.is_cuda) else None
         if side is None:

@@ -68,7 +68,8 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         self.layers = torch.nn.ModuleList([layer(node_ft_irreps)])
         for _ in range(self.num_interactions - 1):
             self.layers.append(layer(hidden))
-        self.nonlin_readout = GeneralNonLinearReadoutBlock(hidden, hidden, readout_irreps)
+        self.nonlin_readout = GeneralNonLinearReadoutBlock(hidden, hidden, readout_irreps,
+                                                           gate=torch.nn.functional.silu)
         self.global_reduction = params.global_reduction
         self.linear = Linear(readout_irreps, Irreps("2x0e+2x2e+1x4e"), biases=True)
         self.sph_to_cart = Spherical_to_Cartesian()

@@ -28,6 +28,14 @@ LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "64"))
 GATE_FUSED = os.environ.get("EELG_GATE_FUSED", "1") != "0"
 
 
+def _output_mask(irreps_out, covered) -> torch.Tensor:
+    """e3nn 0.5 ``output_mask``: 1 on the output irreps some instruction writes, else 0."""
+    if not irreps_out.dim:
+        return torch.ones(0)
+    return torch.cat([torch.full((mul * ir.dim,), 1.0 if o in covered else 0.0)
+                      for o, (mul, ir) in enumerate(irreps_out)])
+
+
 def _accept_output_mask(state_dict, key: str, irreps_out, covered, error_msgs) -> None:
     """e3nn's ``Linear`` / ``TensorProduct`` register an ``output_mask`` buffer (1 on the output
     irreps some instruction writes).  Reference checkpoints may carry it: it is derived data,
@@ -35,10 +43,27 @@ def _accept_output_mask(state_dict, key: str, irreps_out, covered, error_msgs) -
     m = state_dict.pop(key, None)
     if m is None:
         return
-    want = torch.cat([torch.full((mul * ir.dim,), 1.0 if o in covered else 0.0)
-                      for o, (mul, ir) in enumerate(irreps_out)]) if irreps_out.dim else torch.ones(0)
+    want = _output_mask(irreps_out, covered)
     if tuple(m.shape) != tuple(want.shape) or not torch.equal(m.detach().cpu().float() != 0, want != 0):
         error_msgs.append(f"{key}: output mask does not match the module's instructions")
+
+
+def _accept_empty(state_dict, key: str, error_msgs) -> None:
+    """e3nn registers ``torch.Tensor()`` placeholders (``register_buffer('weight' | 'bias',
+    torch.Tensor())``) where a module has no internal weight / bias: a ``TensorProduct`` with
+    external weights, a bias-less ``Linear``, the Gate's ``ElementwiseTensorProduct``.  They
+    are accepted when empty; anything else would be a weight this module does not have."""
+    t = state_dict.pop(key, None)
+    if t is not None and t.numel() != 0:
+        error_msgs.append(f"{key}: expected e3nn's empty placeholder buffer, got shape "
+                          f"{tuple(t.shape)}")
+
+
+def _emit_e3nn_buffers(state_dict, prefix: str, entries) -> None:
+    """``state_dict()`` carries e3nn's derived buffers (output masks, empty placeholders) under
+    the reference's names, so a checkpoint of this model loads strictly into the reference."""
+    for name, t in entries:
+        state_dict[prefix + name] = t
 
 
 class _OnStream(torch.autograd.Function):
@@ -128,11 +153,25 @@ class Linear(torch.nn.Module):
             self.register_parameter("bias", None)
         self._in_off, self._out_off = self.irreps_in.offsets(), self.irreps_out.offsets()
         self._build_descriptors()
+        self._register_state_dict_hook(Linear._emit_derived)
+
+    def _covered(self):
+        # e3nn 0.5 masks by the weight instructions only (not the bias instructions)
+        return {o for _, o in self.instructions}
+
+    @staticmethod
+    def _emit_derived(module, state_dict, prefix, local_metadata):
+        ents = [("output_mask", _output_mask(module.irreps_out, module._covered()))]
+        if module.bias is None:
+            ents.append(("bias", torch.Tensor()))
+        _emit_e3nn_buffers(state_dict, prefix, ents)
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
         _accept_output_mask(state_dict, prefix + "output_mask", self.irreps_out,
-                            {o for _, o in self.instructions}, error_msgs)
+                            self._covered(), error_msgs)
+        if self.bias is None:
+            _accept_empty(state_dict, prefix + "bias", error_msgs)
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
@@ -312,12 +351,22 @@ class Gate(torch.nn.Module):
         self.irreps_in = self.irreps_scalars + self.irreps_gates + self.irreps_gated
         self.irreps_out = self.irreps_scalars + self.irreps_gated
         self.cst = cg.silu_normalize2mom()
+        self._register_state_dict_hook(Gate._emit_derived)
+
+    # e3nn's Gate multiplies with an ElementwiseTensorProduct submodule ``mul`` (external
+    # weights: an empty ``weight`` placeholder, and an output mask over the gated irreps)
+    @staticmethod
+    def _emit_derived(module, state_dict, prefix, local_metadata):
+        g = module.irreps_gated
+        _emit_e3nn_buffers(state_dict, prefix, [
+            ("mul.weight", torch.Tensor()),
+            ("mul.output_mask", _output_mask(g, set(range(len(g)))))])
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
-        # e3nn's Gate multiplies with an ElementwiseTensorProduct submodule ``mul``
         _accept_output_mask(state_dict, prefix + "mul.output_mask", self.irreps_gated,
                             set(range(len(self.irreps_gated))), error_msgs)
+        _accept_empty(state_dict, prefix + "mul.weight", error_msgs)
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
 
@@ -366,10 +415,19 @@ class TensorProduct(torch.nn.Module):
         self.instructions = list(instructions)
         self.weight_numel = sum(self.irreps_in1[i1].mul * self.irreps_in2[i2].mul
                                 for i1, i2, *_ in self.instructions)
+        self._register_state_dict_hook(TensorProduct._emit_derived)
+
+    # external (per-edge) weights: e3nn holds an empty ``weight`` placeholder buffer
+    @staticmethod
+    def _emit_derived(module, state_dict, prefix, local_metadata):
+        _emit_e3nn_buffers(state_dict, prefix, [
+            ("weight", torch.Tensor()),
+            ("output_mask", _output_mask(module.irreps_out, {ins[2] for ins in module.instructions}))])
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
         _accept_output_mask(state_dict, prefix + "output_mask", self.irreps_out,
                             {ins[2] for ins in self.instructions}, error_msgs)
+        _accept_empty(state_dict, prefix + "weight", error_msgs)
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)

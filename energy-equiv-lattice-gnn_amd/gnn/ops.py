@@ -243,23 +243,61 @@ def graph_pool(src, batch, num_graphs: int, reduce: str = "mean"):
     elif reduce in ("sum", "add"):
         inv = torch.ones(num_graphs, device=src.device, dtype=torch.float32)
     elif reduce in ("max", "min", "mul"):
-        return segment_pool_order(src, cnt, reduce)
+        return segment_pool_order(src, ptr, num_graphs, reduce)
     else:
         raise ValueError(f"global_reduction {reduce!r} not supported "
                          "(torch_scatter reduces: sum, add, mean, max, min, mul)")
     return _SegmentMean.apply(src, ptr, batch, inv)
 
 
-def segment_pool_order(src, cnt, reduce: str):
-    """torch_scatter ``scatter(..., reduce='max'|'min'|'mul')`` over sorted per-graph segments
-    of lengths ``cnt`` (``gnn/model.py:100-106`` passes any torch_scatter reduce).  Empty
-    graphs give 0 for max / min (torch_scatter fills untouched rows with 0) and 1 for mul
-    (its output starts at ones).  Readout tail, off the hot path: torch's segment_reduce
-    (one kernel, with autograd) on the pooled [N, 21] rows."""
-    if reduce == "mul":
-        return torch.segment_reduce(src, "prod", lengths=cnt, axis=0, unsafe=True, initial=1.0)
-    out = torch.segment_reduce(src, reduce, lengths=cnt, axis=0, unsafe=True)
-    return torch.where((cnt > 0)[:, None], out, torch.zeros((), dtype=out.dtype, device=out.device))
+_ORDER_OPS = {"max": 0, "min": 1, "mul": 2}
+
+
+class _SegmentOrder(torch.autograd.Function):
+    """torch_scatter ``scatter(..., reduce='max'|'min'|'mul')`` over CSR segments of ``src``
+    rows (``eelg_segment_order``).  max / min: the first extreme of a segment is kept and the
+    whole gradient goes to it (torch_scatter's scatter_max / scatter_min arg); empty segments
+    give 0 (max / min) or 1 (mul), as torch_scatter fills rows that receive nothing."""
+
+    @staticmethod
+    def forward(ctx, src, rowptr, n_rows: int, op: int, covered: bool):
+        src = _f32(src)
+        width = src.shape[1]
+        out = torch.empty(n_rows, width, device=src.device, dtype=torch.float32)
+        arg = (torch.empty(n_rows, width, device=src.device, dtype=torch.int32)
+               if op != _ORDER_OPS["mul"] else None)
+        _lib.check(_lib.load().eelg_segment_order(_lib.ptr(src), _lib.ptr(rowptr), n_rows, width,
+                                                  op, _lib.ptr(out), _lib.ptr(arg),
+                                                  _lib.stream(out)), "segment_order")
+        ctx.save_for_backward(src, rowptr, arg)
+        ctx.n_rows, ctx.op, ctx.covered = n_rows, op, covered
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        src, rowptr, arg = ctx.saved_tensors
+        g = _f32(g)
+        # every row of every segment is written; rows outside all segments must read 0
+        gs = torch.empty_like(src) if ctx.covered else torch.zeros_like(src)
+        _lib.check(_lib.load().eelg_segment_order_bwd(
+            _lib.ptr(src), _lib.ptr(rowptr), _lib.ptr(arg), _lib.ptr(g), ctx.n_rows, src.shape[1],
+            ctx.op, _lib.ptr(gs), _lib.stream(gs)), "segment_order_bwd")
+        return gs, None, None, None, None
+
+
+def segment_order(src, rowptr32, n_rows: int, reduce: str, covered: bool = False):
+    """``reduce`` in max / min / mul over the CSR segments ``rowptr32`` (int32, [n_rows + 1]).
+    ``covered``: the segments cover every row of ``src`` (the backward then skips a zero fill)."""
+    _require_device(src)
+    if reduce not in _ORDER_OPS:
+        raise ValueError(f"segment_order: reduce {reduce!r} (max, min, mul)")
+    return _SegmentOrder.apply(src, rowptr32, n_rows, _ORDER_OPS[reduce], covered)
+
+
+def segment_pool_order(src, ptr32, num_graphs: int, reduce: str):
+    """Per-graph max / min / mul pool (``gnn/model.py:100-106`` passes any torch_scatter
+    reduce) over the sorted ``batch`` segments ``ptr32``."""
+    return segment_order(src, ptr32, num_graphs, reduce)
 
 
 # ---------------------------------------------------------------------------
@@ -280,12 +318,13 @@ class _TPInteraction(torch.autograd.Function):
                              f"w {tuple(w.shape)} vs config {info}")
         if sh.shape[0] != csr.num_edges or w.shape[0] != csr.num_edges or n != csr.num_nodes:
             raise ValueError("edge/node counts do not match the CSR")
-        agg = torch.empty(n, info["dmid"], device=x.device, dtype=torch.float32)
+        n_out = csr.rowptr.shape[0] - 1        # receivers (nodes; edges for per_edge_csr)
+        agg = torch.empty(n_out, info["dmid"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
         tok = TIMER.start(f"tp_fwd[din={info['din']}]")
         fwd = lib.eelg_tp_fwd_bf16 if bf else lib.eelg_tp_fwd
         _lib.check(fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
-                       _lib.ptr(csr.rowptr), n, float(inv_norm), _lib.ptr(agg), _lib.stream(agg)),
+                       _lib.ptr(csr.rowptr), n_out, float(inv_norm), _lib.ptr(agg), _lib.stream(agg)),
                    "tp_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, sh, w)
@@ -328,6 +367,32 @@ class _TPInteraction(torch.autograd.Function):
 def tp_interaction(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
     _require_device(x, sh, w)
     return _TPInteraction.apply(x, sh, w, csr, cfg, info, inv_norm)
+
+
+def per_edge_csr(csr: EdgeCSR) -> EdgeCSR:
+    """The same edges with every edge its own receiver segment (``rowptr = 0..E``,
+    ``receiver = e``): ``tp_interaction`` over it returns the per-edge messages
+    ``conv_tp(x[sender], sh, w) * inv_norm`` as ``[E, dmid]`` rows in receiver-sorted order, and
+    its backward reads one grad row per edge.  The sender CSR (grad-x) is the base graph's.
+    Cached on ``csr``."""
+    pe = getattr(csr, "_per_edge", None)
+    if pe is None:
+        e = csr.num_edges
+        ar = torch.arange(e + 1, device=csr.rowptr.device, dtype=torch.int32)
+        pe = EdgeCSR(csr.perm, csr.sender, ar[:e], ar, csr.sperm, csr.srowptr, csr.num_nodes)
+        csr._per_edge = pe
+    return pe
+
+
+def in_degree_scale(csr: EdgeCSR) -> torch.Tensor:
+    """[N] fp32 ``1 / max(in-degree, 1)`` (torch_scatter 'mean' divides by the clamped count);
+    cached on ``csr``."""
+    s = getattr(csr, "_inv_deg", None)
+    if s is None:
+        deg = (csr.rowptr[1:] - csr.rowptr[:-1]).to(torch.float32)
+        s = 1.0 / deg.clamp_min(1.0)
+        csr._inv_deg = s
+    return s
 
 
 # ---------------------------------------------------------------------------
@@ -471,11 +536,23 @@ def _radial_desc(params, n_feat: int):
     return d
 
 
+def _radial_chunks(e: int, n_out: int, out_es: int, hidden: int, n_hidden: int):
+    """Edge ranges under the radial kernels' 2 GiB per-stream limit (their buffer descriptors
+    use 32-bit byte offsets): ``E * n_out * out_es`` for the [E, W] output / its gradient and
+    ``E * hidden * n_hidden * 4`` for the saved pre-activations.  One range below the limit."""
+    per_edge = max(n_out * out_es, hidden * n_hidden * 4, 1)
+    cap = ((1 << 31) - 1) // per_edge // 128 * 128
+    if cap <= 0:
+        raise ValueError(f"radial MLP: one edge row ({per_edge} B) exceeds the 2 GiB stream limit")
+    return [(a, min(a + cap, e)) for a in range(0, e, cap)] or [(0, 0)]
+
+
 class _RadialMLP(torch.autograd.Function):
     """Linear(+bias)-SiLU-...-Linear(no bias) on edge features as one fused HIP kernel
     (``eelg_radial_fwd``: fp32 MFMA, hidden activations in LDS, only the pre-activations
     and the [E, W] output reach HBM), backward as two (``eelg_radial_bwd``).  No grad w.r.t.
-    the features, which come from eelg_edge_embed without grad."""
+    the features, which come from eelg_edge_embed without grad.  Edge sets past
+    the kernels' 2 GiB per-stream limit run as several launches (``_radial_chunks``)."""
 
     @staticmethod
     def forward(ctx, feats, out_dtype, *params):
@@ -487,44 +564,57 @@ class _RadialMLP(torch.autograd.Function):
         wo = params[-1]
         if wo.shape[1] != d.hidden or any(p.shape[0] != d.hidden for p in params[:-1]):
             raise ValueError("radial MLP: hidden widths differ between layers")
-        zsave = torch.empty(d.n_hidden, e, d.hidden, device=feats.device, dtype=torch.float32)
         out = torch.empty(e, d.n_out, device=feats.device, dtype=out_dtype)
         wo_t = wo.t().contiguous()
         lib = _lib.load()
-        _lib.check(lib.eelg_radial_fwd(_lib.ptr(feats), e, ctypes.byref(d), _lib.ptr(wo_t),
-                                       int(out_dtype == torch.bfloat16), _lib.ptr(zsave),
-                                       _lib.ptr(out), _lib.stream(feats)), "radial_fwd")
-        ctx.save_for_backward(feats, zsave, *params)
+        chunks = _radial_chunks(e, d.n_out, out.element_size(), d.hidden, d.n_hidden)
+        zs = []
+        for a, b in chunks:
+            z = torch.empty(d.n_hidden, b - a, d.hidden, device=feats.device, dtype=torch.float32)
+            _lib.check(lib.eelg_radial_fwd(_lib.ptr(feats[a:b]), b - a, ctypes.byref(d),
+                                           _lib.ptr(wo_t), int(out_dtype == torch.bfloat16),
+                                           _lib.ptr(z), _lib.ptr(out[a:b]), _lib.stream(feats)),
+                       "radial_fwd")
+            zs.append(z)
+        ctx.chunks = chunks
+        ctx.save_for_backward(feats, *params, *zs)
+        ctx.n_params = len(params)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        feats, zsave, *params = ctx.saved_tensors
+        feats, *rest = ctx.saved_tensors
+        params, zs = rest[:ctx.n_params], rest[ctx.n_params:]
         g = g.contiguous()
         e, nf = feats.shape
         d = _radial_desc(params, nf)
         lib = _lib.load()
-        npart, ns = ctypes.c_int(), ctypes.c_int()
-        _lib.check(lib.eelg_radial_plan(e, d.n_out, ctypes.byref(npart), ctypes.byref(ns)),
-                   "radial_plan")
         h = d.hidden
         n_small = h * nf + h + (d.n_hidden - 1) * (h * h + h)
-        part_h = torch.empty(npart.value, n_small, device=g.device, dtype=torch.float32)
-        part_wo = torch.empty(ns.value, d.n_out, h, device=g.device, dtype=torch.float32)
-        grad_h = torch.empty(e, h, device=g.device, dtype=torch.float32)
-        if e == 0:
-            part_h.zero_()
-            part_wo.zero_()
-        _lib.check(lib.eelg_radial_bwd(_lib.ptr(g), int(g.dtype == torch.bfloat16), e,
-                                       ctypes.byref(d), _lib.ptr(params[-1]), _lib.ptr(zsave),
-                                       _lib.ptr(feats), _lib.ptr(grad_h), _lib.ptr(part_h),
-                                       _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
-        small = part_h.sum(0)
+        small, gwo = None, None
+        for (a, b), z in zip(ctx.chunks, zs):
+            ec = b - a
+            npart, ns = ctypes.c_int(), ctypes.c_int()
+            _lib.check(lib.eelg_radial_plan(ec, d.n_out, ctypes.byref(npart), ctypes.byref(ns)),
+                       "radial_plan")
+            part_h = torch.empty(npart.value, n_small, device=g.device, dtype=torch.float32)
+            part_wo = torch.empty(ns.value, d.n_out, h, device=g.device, dtype=torch.float32)
+            grad_h = torch.empty(ec, h, device=g.device, dtype=torch.float32)
+            if ec == 0:
+                part_h.zero_()
+                part_wo.zero_()
+            _lib.check(lib.eelg_radial_bwd(_lib.ptr(g[a:b]), int(g.dtype == torch.bfloat16), ec,
+                                           ctypes.byref(d), _lib.ptr(params[-1]), _lib.ptr(z),
+                                           _lib.ptr(feats[a:b]), _lib.ptr(grad_h), _lib.ptr(part_h),
+                                           _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
+            sm, wo = part_h.sum(0), part_wo.sum(0)
+            small = sm if small is None else small + sm
+            gwo = wo if gwo is None else gwo + wo
         grads, off = [], 0
         for p in params[:-1]:
             grads.append(small[off: off + p.numel()].view_as(p))
             off += p.numel()
-        grads.append(part_wo.sum(0))
+        grads.append(gwo)
         return (None, None, *grads)
 
 

@@ -29,7 +29,9 @@ class FlatGradAllReduce:
 
     Packing is one ``torch.cat`` and unpacking one ``_foreach_copy_`` (a handful of
     launches instead of two copies per parameter), so the exchange costs one RCCL
-    all-reduce plus O(1) kernels per step.  Missing gradients count as zeros."""
+    all-reduce plus O(1) kernels per step.  A parameter without a gradient on this rank
+    contributes zeros (one cached zero tensor, no per-step fill) and receives the averaged
+    slice as a view of the reduced buffer."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
@@ -42,14 +44,27 @@ class FlatGradAllReduce:
         world = dist.get_world_size(self.group)
         if world == 1 or not self.params:
             return
+        if not hasattr(self, "_zeros"):
+            self._zeros = {}
+        parts = []
         for p in self.params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        grads = [p.grad for p in self.params]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+            if p.grad is not None:
+                parts.append(p.grad.reshape(-1))
+            else:
+                z = self._zeros.get(id(p))
+                if z is None or z.device != p.device:
+                    z = self._zeros[id(p)] = torch.zeros(p.numel(), device=p.device, dtype=p.dtype)
+                parts.append(z)
+        flat = torch.cat(parts)
         dist.all_reduce(flat, group=self.group)
         flat.div_(world)
-        torch._foreach_copy_(grads, [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)])
+        views = flat.split([p.numel() for p in self.params])
+        have = [(p.grad, v.view_as(p)) for p, v in zip(self.params, views) if p.grad is not None]
+        if have:
+            torch._foreach_copy_([g for g, _ in have], [v for _, v in have])
+        for p, v in zip(self.params, views):
+            if p.grad is None:
+                p.grad = v.view_as(p)
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:

@@ -18,8 +18,9 @@ from torch import Tensor
 from . import _lib, ops
 
 
-def _csr(sender, receiver, rowptr, sperm, srowptr) -> "ops.EdgeCSR":
-    return ops.EdgeCSR(sender, sender, receiver, rowptr, sperm, srowptr, int(rowptr.shape[0]) - 1)
+def _csr(sender, receiver, rowptr, sperm, srowptr, n_nodes=None) -> "ops.EdgeCSR":
+    n = int(srowptr.shape[0]) - 1 if n_nodes is None else n_nodes    # x rows (sender CSR)
+    return ops.EdgeCSR(sender, sender, receiver, rowptr, sperm, srowptr, n)
 
 
 def _info(cfg: int):
@@ -39,7 +40,7 @@ def tp_interaction(x: Tensor, sh: Tensor, w: Tensor, sender: Tensor, receiver: T
 
 @tp_interaction.register_fake
 def _(x, sh, w, sender, receiver, rowptr, sperm, srowptr, cfg, inv_norm):
-    return x.new_empty(x.shape[0], _info(cfg)["dmid"], dtype=torch.float32)
+    return x.new_empty(rowptr.shape[0] - 1, _info(cfg)["dmid"], dtype=torch.float32)
 
 
 @torch.library.custom_op("eelg::tp_interaction_bwd", mutates_args=(), device_types="cuda")
@@ -84,6 +85,25 @@ def segment_sum_csr(src: Tensor, rowptr: Tensor, scale: float = 1.0) -> Tensor:
 @segment_sum_csr.register_fake
 def _(src, rowptr, scale=1.0):
     return src.new_empty((rowptr.shape[0] - 1,) + tuple(src.shape[1:]), dtype=torch.float32)
+
+
+def _seg_setup(ctx, inputs, output):
+    src, rowptr, scale = inputs
+    ctx.save_for_backward(rowptr)
+    ctx.n_src, ctx.scale = src.shape[0], scale
+
+
+def _seg_backward(ctx, g):
+    """grad src[j] = scale * g[row of j]; rows outside every segment get 0."""
+    (rowptr,) = ctx.saved_tensors
+    j = torch.arange(ctx.n_src, device=g.device, dtype=torch.int64)
+    row = torch.searchsorted(rowptr[1:].to(torch.int64), j, right=True)
+    j0 = (j >= rowptr[0].to(torch.int64)).to(g.dtype).view(-1, *([1] * (g.dim() - 1)))
+    gpad = torch.cat([g, g.new_zeros((1,) + tuple(g.shape[1:]))])     # row n: outside
+    return gpad[row] * j0 * ctx.scale, None, None
+
+
+segment_sum_csr.register_autograd(_seg_backward, setup_context=_seg_setup)
 
 
 class _Ctx:

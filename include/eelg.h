@@ -144,6 +144,22 @@ int eelg_segment_sum_split(const float* src, const int* rowptr, const int* idx,
                            const float* row_scale, float scale, int n_rows, int width, int n_split,
                            float* work, float* out, void* stream);
 
+/* torch_scatter's order reductions over CSR segments of src rows (rows rowptr[r]..rowptr[r+1]):
+ * op 0 = max, 1 = min, 2 = mul.  Replaces scatter(..., reduce='max'|'min'|'mul') for
+ * interaction_reduction (gnn/blocks.py:595-597, on the per-edge messages in receiver order)
+ * and global_reduction (gnn/model.py:100-106, on the readout rows in graph order).
+ * out[r, c]: the segment's first maximum / minimum (strict compare, so ties keep the earliest
+ * row, torch_scatter's CPU arg) or its product; an empty segment gives 0 (max / min) or 1 (mul).
+ * arg[r, c] (max / min only, required): the row of the kept element, -1 for an empty segment. */
+int eelg_segment_order(const float* src, const int* rowptr, int n_rows, int width, int op,
+                       float* out, int* arg, void* stream);
+/* Backward: grad_src for every row of every segment (rows outside all segments are not
+ * written): max / min -> grad_out at arg, 0 elsewhere (the whole gradient to one element, as
+ * torch_scatter's scatter_max / scatter_min); mul -> grad_out times the product of the
+ * segment's other entries (prefix x suffix products, exact at zeros). */
+int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, const float* grad_out,
+                           int n_rows, int width, int op, float* grad_src, void* stream);
+
 /* Crystal-graph edge convolution (CGC/mCGC benchmark models): replaces
  *   c = cat([x[sender], x[receiver], edge_ft]); msg = softplus(fc_values(c)) * sigmoid(fc_multip(c));
  *   scatter(msg, receiver, reduce)          (scripts/benchmark_models/cgc_modified.py:20-25,

@@ -149,7 +149,7 @@ class EquivariantProductBlock(torch.nn.Module):
 
 
 class TensorProductInteractionBlock(torch.nn.Module):
-    """``gnn/blocks.py:495-604`` (reduce='sum')."""
+    """``gnn/blocks.py:495-604``; ``reduce`` is any torch_scatter reduce (``:595-597``)."""
 
     def __init__(self, node_feats_irreps, edge_attrs_irreps, edge_feats_irreps, irreps_out,
                  agg_norm_const, reduce="sum", bias=False, MLP_dim=64, MLP_layers=3):
@@ -160,7 +160,7 @@ class TensorProductInteractionBlock(torch.nn.Module):
         self._irreps_out = o3.Irreps(irreps_out)
         self.agg_norm_const = agg_norm_const
         self.reduce = reduce.lower()
-        assert self.reduce == "sum", "only interaction_reduction='sum' is on the hot path"
+        assert self.reduce in ("sum", "add", "mean", "max", "min", "mul"), self.reduce
         self.linear_up = o3.Linear(self._node_feats_irreps, self._node_feats_irreps)
         irreps_mid, instructions = tp_out_irreps_with_instructions(
             self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
@@ -187,7 +187,13 @@ class TensorProductInteractionBlock(torch.nn.Module):
         node_feats = self.linear_up(node_feats)
         tp_weights = self.conv_tp_weights(edge_feats)
         mji = self.conv_tp(node_feats[sender], edge_attrs, tp_weights)
-        message = scatter_sum(mji, receiver, n) / self.agg_norm_const
+        if self.reduce in ("sum", "add"):
+            message = scatter_sum(mji, receiver, n)
+        elif self.reduce == "mean":
+            message = scatter_mean(mji, receiver, n)
+        else:
+            message = scatter_reduce_order(mji, receiver, n, self.reduce)
+        message = message / self.agg_norm_const
         return self.linear(message), None
 
 

@@ -103,17 +103,101 @@ def test_loaded_Q_flat_is_used():
     assert torch.equal(m.stiffness_head.sph_to_cart.Q_flat, sd["stiffness_head.sph_to_cart.Q_flat"])
 
 
-def test_e3nn_output_masks_are_accepted():
-    """e3nn's Linear / TensorProduct / Gate carry derived ``output_mask`` buffers."""
+# e3nn 0.5's derived buffers in a reference checkpoint (gnn/blocks.py:516-535,553-559,268-279):
+# output masks of every Linear / TensorProduct / the Gate's ElementwiseTensorProduct, empty
+# ``weight`` placeholders of the external-weight tensor products, empty ``bias`` placeholders
+# of the bias-less Linears
+E3NN_KEYS = {
+    "stiffness_head.layers.1.interaction.linear_up.output_mask": (800,),
+    "stiffness_head.layers.1.interaction.linear_up.bias": (0,),
+    "stiffness_head.layers.1.interaction.conv_tp.output_mask": (7360,),
+    "stiffness_head.layers.1.interaction.conv_tp.weight": (0,),
+    "stiffness_head.layers.1.interaction.linear.output_mask": (800,),
+    "stiffness_head.layers.1.product.linear.output_mask": (800,),
+    "stiffness_head.layers.1.product.linear.bias": (0,),
+    "stiffness_head.layers.0.interaction.conv_tp.weight": (0,),
+    "stiffness_head.nonlin_readout.linear_1.bias": (0,),
+    "stiffness_head.nonlin_readout.linear_2.bias": (0,),
+    "stiffness_head.nonlin_readout.equivariant_nonlin.mul.output_mask": (768,),
+    "stiffness_head.nonlin_readout.equivariant_nonlin.mul.weight": (0,),
+    "stiffness_head.linear.output_mask": (21,),
+}
+
+
+def test_e3nn_buffers_are_emitted_and_accepted():
+    """Both the oracle (the stand-in for a reference checkpoint) and the product carry every
+    e3nn derived buffer under the reference's names; a strict load accepts them."""
+    o, m = _pair(2, 4)
+    so, sm = o.state_dict(), m.state_dict()
+    for k, shape in E3NN_KEYS.items():
+        assert tuple(so[k].shape) == shape, k
+        assert tuple(sm[k].shape) == shape, k
+        assert torch.equal(so[k], sm[k].to(so[k].dtype)), k
+    m.load_state_dict(so, strict=True)
+    o.load_state_dict(sm, strict=True)
+
+
+def test_e3nn_output_masks_are_verified():
     o, m = _pair(2, 4)
     sd = o.state_dict()
-    sd["stiffness_head.layers.1.interaction.linear_up.output_mask"] = torch.ones(800)
-    sd["stiffness_head.layers.1.interaction.conv_tp.output_mask"] = torch.ones(7360)
-    sd["stiffness_head.nonlin_readout.equivariant_nonlin.mul.output_mask"] = torch.ones(768)
-    m.load_state_dict(sd, strict=True)
     sd["stiffness_head.layers.1.interaction.linear.output_mask"] = torch.zeros(800)
     with pytest.raises(RuntimeError, match="output mask"):
         m.load_state_dict(sd, strict=True)
+
+
+@pytest.mark.parametrize("key", ["stiffness_head.layers.1.interaction.conv_tp.weight",
+                                 "stiffness_head.layers.1.interaction.linear_up.bias",
+                                 "stiffness_head.nonlin_readout.equivariant_nonlin.mul.weight"])
+def test_e3nn_placeholders_must_be_empty(key):
+    o, m = _pair(2, 4)
+    sd = o.state_dict()
+    sd[key] = torch.ones(3)
+    with pytest.raises(RuntimeError, match="placeholder"):
+        m.load_state_dict(sd, strict=True)
+
+
+def test_standard_checkpoint_after_rotated_one_restores_the_derived_basis():
+    """loading a checkpoint with U in another basis, then a standard one, must
+    compute with the derived U again (and save it)."""
+    o, m = _pair(2, 4)
+    std = o.state_dict()
+    sc_key = "stiffness_head.layers.1.product.symmetric_contractions"
+    m.load_state_dict(std, strict=True)
+    sc = m.stiffness_head.layers[1].product.symmetric_contractions
+    coef_std = sc.coefficients().detach().clone()
+    u_std = sc.u_sym.clone()
+    rot = {k: v.clone() for k, v in std.items()}
+    _rotate_U_basis(rot, f"{sc_key}.contractions.32x2e", 3, 1)
+    m.load_state_dict(rot, strict=True)
+    assert len(sc._u_loaded) == 1 and not torch.equal(sc.u_sym, u_std)
+    m.load_state_dict(std, strict=True)
+    assert sc._u_loaded == {}
+    assert torch.equal(sc.u_sym, u_std)
+    assert torch.equal(sc.coefficients().detach(), coef_std)
+    key = f"{sc_key}.contractions.32x2e.U_matrix_3"
+    assert torch.allclose(m.state_dict()[key].double(), std[key].double(), atol=1e-7)
+
+
+def test_failed_U_load_leaves_the_basis_untouched():
+    o, m = _pair(2, 4)
+    sd = o.state_dict()
+    sc = m.stiffness_head.layers[1].product.symmetric_contractions
+    u0 = sc.u_sym.clone()
+    sc_key = "stiffness_head.layers.1.product.symmetric_contractions.contractions"
+    _rotate_U_basis(sd, f"{sc_key}.32x2e", 3, 1)                     # adoptable
+    sd[f"{sc_key}.32x4e.U_matrix_1"] = torch.zeros(3, 3)               # bad shape
+    with pytest.raises(RuntimeError):
+        m.load_state_dict(sd, strict=True)
+    assert torch.equal(sc.u_sym, u0)
+
+
+def test_checkpoint_without_mandel_tables_loads():
+    """checkpoints written before Cart_4_to_Mandel registered its tables."""
+    o, m = _pair(2, 4)
+    sd = m.state_dict()
+    for name in ("mask", "rows", "cols"):
+        del sd[f"stiffness_head.cart_to_Mandel.{name}"]
+    m.load_state_dict(sd, strict=True)
 
 
 def test_reference_U_shapes():

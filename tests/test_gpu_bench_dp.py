@@ -1,0 +1,53 @@
+"""BASELINE config 3's entry point: ``bench.py --gpus 2`` through its own spawn launcher.
+
+The bench runs as a fresh child process (its launcher starts the two rank processes before
+anything touches the GPU), 2 ranks x 32 graphs x 1024 nodes, 3 timed AdamW steps.  With
+two visible GPUs the ranks talk over RCCL ('nccl'); on a one-GPU box they share the device
+over gloo, which the bench refuses unless ``--rehearsal`` is given (and then labels the
+line).  Checked on the JSON line: ranks 2, ``graph-sharded dp2``, global batch 64, a finite
+value, the backend named, and bitwise-equal parameters on both ranks after the steps
+(``--check-params``: an elementwise max == min all-reduce over every parameter).
+"""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra, timeout=300):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--no-cpu-baseline", *extra]
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_two_ranks_reports_dp2_and_keeps_replicas_identical():
+    ndev = torch.cuda.device_count()
+    extra = ["--check-params"] + ([] if ndev >= 2 else ["--rehearsal"])
+    r = _run(*extra)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["ranks"] == 2
+    assert out["config"]["parallelism"] == "graph-sharded dp2"
+    assert out["config"]["global_batch"] == 64
+    assert math.isfinite(out["value"]) and out["value"] > 0
+    assert out["backend"] == ("nccl" if ndev >= 2 else "gloo")
+    assert out["rehearsal"] == (ndev < 2)
+    assert out["params_equal_across_ranks"] is True
+    assert math.isfinite(out["loss"])
+
+
+def test_bench_refuses_a_multi_rank_headline_over_gloo():
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs visible: the bench runs RCCL, nothing to refuse")
+    r = _run(timeout=200)
+    assert r.returncode != 0
+    assert "refusing" in (r.stderr + r.stdout)

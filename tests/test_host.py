@@ -243,27 +243,6 @@ def test_storage_dtype_param_validation():
         storage_dtype(params(2, storage_dtype="fp8"))
 
 
-@pytest.mark.parametrize("reduce", ["max", "min", "mul"])
-def test_segment_pool_order_matches_oracle(reduce):
-    """ops.segment_pool_order (global_reduction max / min / mul, gnn/model.py:100-106) vs the
-    oracle's torch_scatter restatement, with an empty graph; values and gradients, fp64."""
-    from gnn import ops
-    from oracle.blocks import scatter_reduce_order
-    torch.manual_seed(3)
-    sizes = torch.tensor([3, 0, 5, 1])
-    idx = torch.repeat_interleave(torch.arange(4), sizes)
-    src = torch.rand(int(sizes.sum()), 21, dtype=torch.float64) + 0.5
-    a = src.clone().requires_grad_(True)
-    b = src.clone().requires_grad_(True)
-    out = ops.segment_pool_order(a, sizes, reduce)
-    ref = scatter_reduce_order(b, idx, 4, reduce)
-    g = torch.randn_like(ref)
-    (out * g).sum().backward()
-    (ref * g).sum().backward()
-    assert torch.allclose(out, ref, rtol=1e-12, atol=0)
-    assert torch.allclose(a.grad, b.grad, rtol=1e-12, atol=1e-15)
-
-
 def test_torch_library_ops_fake_shapes():
     """torch.ops.eelg.* (dispatcher-visible form of the fused interaction) propagate
     shapes and dtypes on meta tensors without running HIP code."""
@@ -284,3 +263,40 @@ def test_torch_library_ops_fake_shapes():
     assert gx.shape == (n, info["din"]) and gx.dtype == torch.float32
     assert gw.shape == (e, info["wn"]) and gw.dtype == torch.bfloat16
     assert torch.ops.eelg.segment_sum_csr(meta(e, 7), meta(n + 1, dt=torch.int32)).shape == (n, 7)
+
+
+def test_readout_gate_other_than_silu_raises():
+    """``GeneralNonLinearReadoutBlock(gate=...)`` (gnn/blocks.py:256,270-272): the fused Gate is
+    SiLU; another activation raises instead of being replaced silently."""
+    from gnn.blocks import GeneralNonLinearReadoutBlock
+    hid = "32x0e+32x1o+32x2e"
+    for g in (None, torch.nn.functional.silu, torch.nn.SiLU()):
+        GeneralNonLinearReadoutBlock(hid, hid, "16x0e+16x1o+16x2e", gate=g)
+    with pytest.raises(NotImplementedError, match="SiLU"):
+        GeneralNonLinearReadoutBlock(hid, hid, "16x0e+16x1o+16x2e", gate=torch.tanh)
+
+
+def test_interaction_reductions_are_accepted_and_pna_is_not():
+    from gnn.blocks import TensorProductInteractionBlock
+    from gnn.irreps import Irreps
+    sh = Irreps.spherical_harmonics(2)
+    hid = "32x0e+32x1o+32x2e"
+    tgt = (sh * 32).sort()[0].simplify()
+    for r in ("sum", "add", "mean", "max", "min", "mul", "MAX"):
+        TensorProductInteractionBlock(hid, sh, "12x0e", tgt, 4.0, r)
+    with pytest.raises(NotImplementedError, match="pna"):
+        TensorProductInteractionBlock(hid, sh, "12x0e", tgt, 4.0, "pna")
+
+
+def test_reshape_irreps_round_trip_matches_reference_layout():
+    """``reshape_irreps`` (gnn/mace.py:316-332) and its inverse, which the product's
+    ``SymmetricContraction.forward`` applies to the reference's [N, mul, 25] input."""
+    from gnn.irreps import Irreps
+    from gnn.mace import reshape_irreps, unreshape_irreps
+    from oracle.mace import reshape_irreps as oreshape
+    ir = Irreps("32x0e+32x1o+32x2e+32x3o+32x4e")
+    x = torch.randn(7, ir.dim, dtype=torch.float64)
+    r = reshape_irreps(ir)(x)
+    assert r.shape == (7, 32, 25)
+    assert torch.equal(r, oreshape("32x0e+32x1o+32x2e+32x3o+32x4e", x))
+    assert torch.equal(unreshape_irreps(ir, r), x)
