@@ -437,7 +437,13 @@ static const eelg_tp_cfg* tp_cfg(int cfg) {
 
 // node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up to a
 // multiple of 8 so every tile's ngroups blocks land on one XCD (see gen_kernels.py)
+// cooperative forward (fwd_tile > 0): one block per fwd_tile receivers, the block count rounded
+// up to a multiple of 8 (XCD k takes a contiguous range of tiles; surplus blocks exit)
 static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes) {
+  if (c.fwd_tile > 0) {
+    const int nb = (n_nodes + c.fwd_tile - 1) / c.fwd_tile;
+    return dim3(((nb + 7) / 8) * 8);
+  }
   const int tiles = (n_nodes + 8 * c.nph - 1) / (8 * c.nph);
   return dim3(((tiles + 7) / 8) * 8 * c.ngroups);
 }
@@ -447,8 +453,8 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x, sh,
-                     w, sender, rowptr, n_nodes, inv_norm, agg);
+  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(c->fwd_threads), 0, (hipStream_t)stream, x,
+                     sh, w, sender, rowptr, n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");
 }
 
@@ -457,8 +463,8 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x,
-                     sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
+  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(c->fwd_threads), 0, (hipStream_t)stream,
+                     x, sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
                      agg);
   return check_launch("tp_fwd_bf16");
 }

@@ -38,6 +38,8 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_bf_fn bwd_bf;
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
+  int fwd_threads;           // tp_fwd block size
+  int fwd_tile;              // cooperative tp_fwd: receivers per block (0: one block per path group and node tile)
 };
 
 struct eelg_sc_cfg {

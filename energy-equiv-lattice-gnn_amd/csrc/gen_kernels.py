@@ -70,6 +70,21 @@ SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
 # slower, r02t); 0: it reads channel-major copies written by sc_bwd_x
 SC_COEF_MULMAJOR = int(os.environ.get("EELG_SC_COEF_MULMAJOR", "0"))
 TP_WPE = int(os.environ.get("EELG_TP_WPE", "0"))     # amdgpu_waves_per_eu floor for tp_fwd (0 = none)
+# tp_fwd with the edge-uniform CG coupling M shared across channels through LDS (emit_tp_fwd_m)
+# and its edge batch (phase-1 lanes per half-wave, a power of two <= 32)
+TP_FWD_M = int(os.environ.get("EELG_TP_FWD_M", "0"))
+TP_M_B = int(os.environ.get("EELG_TP_M_B", "8"))
+TP_NOCOMPUTE = int(os.environ.get("EELG_TP_NOCOMPUTE", "0"))   # diagnostic only: tp_fwd without its CG arithmetic
+TP_M_PAIR = int(os.environ.get("EELG_TP_M_PAIR", "0"))
+# cooperative forward (emit_tp_fwd_coop): edges per tile per batch, receivers per tile, and the
+# accumulator cap of its balanced path groups
+TP_COOP = int(os.environ.get("EELG_TP_COOP", "0"))
+TP_XCD_CONTIG = int(os.environ.get("EELG_TP_XCD_CONTIG", "1"))
+TP_CO_BE = int(os.environ.get("EELG_TP_CO_BE", "4"))
+TP_CO_R = int(os.environ.get("EELG_TP_CO_R", "16"))
+TP_CO_MAXACC = int(os.environ.get("EELG_TP_CO_MAXACC", "36"))
+TP_CO_WPE = int(os.environ.get("EELG_TP_CO_WPE", "0"))       # amdgpu_waves_per_eu floor (0 = none)
+TP_M_AHEAD = int(os.environ.get("EELG_TP_M_AHEAD", "2"))      # coupling chunks read ahead of use
 
 
 fnv1a64 = cg.fnv1a64
@@ -201,10 +216,15 @@ def _emit_acc(p: cg.TPPath, xname, yname, aname, L: List[str], ind: str):
     pairs = sorted({(i, j) for (i, j, k), _ in nz})
     iks = sorted({(i, k) for (i, j, k), _ in nz})
     if len(pairs) <= len(iks):
-        for i, j in pairs:
-            L.append(f"{ind}const float z{i}_{j} = {xname(p, i)} * {yname(p, j)};")
+        # each pair product is followed by the terms using it (short live ranges)
+        byij: Dict[Tuple[int, int], List] = {}
         for (i, j, k), c in nz:
-            L.append(f"{ind}{aname(k)} = fmaf({flit(c)}, z{i}_{j}, {aname(k)});")
+            byij.setdefault((i, j), []).append((k, c))
+        for i, j in pairs:
+            L.append(f"{ind}{{ const float z = {xname(p, i)} * {yname(p, j)};")
+            for k, c in byij[(i, j)]:
+                L.append(f"{ind}  {aname(k)} = fmaf({flit(c)}, z, {aname(k)});")
+            L.append(f"{ind}}}")
     else:
         byik: Dict[Tuple[int, int], List[str]] = {}
         for (i, j, k), c in nz:
@@ -244,13 +264,28 @@ def vec_store(vals: Sequence[str], base: str, start: str) -> List[str]:
 
 
 def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
-    """the needed SH components from a 16-B aligned padded row, one float4 per 4 components"""
+    """The needed SH components from a 16-B aligned padded row: one float4 per fully needed
+    16-B block, narrower loads of exactly the needed runs otherwise.  (A float4 whose lanes are
+    partly unused would leave destination registers the compiler may reuse while the load is
+    in flight, which forces a wait for it: the last row block holds y24 alone at lmax 4.)"""
     need = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
     out = []
     for b in sorted({j // 4 for j in need}):
         comps = [j for j in need if j // 4 == b]
-        out.append(f"{{ const eelg_f4a v_ = *reinterpret_cast<const eelg_f4a*>({base} + {4 * b}); "
-                   + " ".join(f"{pref}y{j} = v_[{j - 4 * b}];" for j in comps) + " }")
+        if len(comps) == 4:
+            out.append(f"{{ const eelg_f4a v_ = *reinterpret_cast<const eelg_f4a*>({base} + {4 * b}); "
+                       + " ".join(f"{pref}y{j} = v_[{j - 4 * b}];" for j in comps) + " }")
+            continue
+        runs, cur = [], [comps[0]]
+        for j in comps[1:]:
+            if j == cur[-1] + 1:
+                cur.append(j)
+            else:
+                runs.append(cur)
+                cur = [j]
+        runs.append(cur)
+        for r in runs:
+            out += vec_load([f"{pref}y{j}" for j in r], base, str(r[0]))
     return out
 
 
@@ -270,7 +305,13 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
     L.append("  const int lane = threadIdx.x & 63;")
     L.append("  const int c0 = (lane & 15) * 2;")
     L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-    L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
+    if TP_XCD_CONTIG:
+        # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the
+        # x rows of a lattice are gathered by one XCD (its L2) rather than by all eight
+        L.append(f"  const int ntl = (n_nodes + {8 * TP_NPH - 1}) / {8 * TP_NPH}, tpx = (ntl + 7) >> 3;")
+        L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    else:
+        L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
     L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4)) * {TP_NPH};")
     L.append("  if (n0 >= n_nodes) return;")
     L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
@@ -362,6 +403,449 @@ def emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off) ->
     return L
 
 
+def _group_entries(grp: List[cg.TPPath]):
+    """The edge-uniform coupling entries of a path group: for every path p and nonzero (i, k)
+    of its CG block, M_p[i, k] = sum_j coef_p * C_ijk * y_j (the path normalisation folded in).
+    Returns [(p, i, k, [(c, j), ...])] in path order; within a path (i, k) order when the path
+    weight is folded into x (d1 <= d3), (k, i) order when it is applied to the path result, so
+    the forward consumes the entries strictly in order (few chunks live at a time)."""
+    ents = []
+    for p in grp:
+        by: Dict[Tuple[int, int], List[Tuple[float, int]]] = {}
+        for (i, j, k), c in _path_cg(p):
+            by.setdefault((i, k), []).append((c * p.coef, p.l2 * p.l2 + j))
+        key = (lambda ik: ik) if 2 * p.l1 + 1 <= 2 * p.l3 + 1 else (lambda ik: (ik[1], ik[0]))
+        for (i, k) in sorted(by, key=key):
+            ents.append((p, i, k, by[(i, k)]))
+    return ents
+
+
+def emit_tp_fwd_m(name, sfx, WT, ld_w, groups, din, nshp, nsh, wn, dmid, node_off) -> List[str]:
+    """Forward with the edge-uniform CG coupling shared across the channels through LDS.
+
+    For an edge, every channel u of path p computes out_k += w_p[u] * sum_i M_p[i,k] x_i[u]
+    with M_p[i,k] = sum_j coef_p C_ijk y_j: M depends on the edge only, so the per-channel
+    form (what the straight-line per-lane code evaluates redundantly in all 32 lanes) costs
+    nnz + (i,k) products per lane, while with M given it costs one FMA per (i,k).
+
+    * Phase 1, every TP_M_B edges: lane s (= lane & (B-1)) of a half-wave evaluates the
+      group's M entries for edge e + s of its stream (straight-line, literal CG constants,
+      inv_norm folded into y) and stores them to the half-wave's LDS slab in chunk-major
+      float4s [chunk][slot][4] (B lanes write B consecutive float4: conflict-free).  The SH
+      rows of the next batch are loaded meanwhile (one row per lane, a batch ahead).
+    * Phase 2, per edge: the 32 lanes (= channels) read the edge's chunks as broadcast
+      ds_read_b128 and apply them to x[sender] with the path weight folded into the shorter
+      of x (d1) or the path result (d3).
+    * TP_M_PAIR: two edges per loop iteration, whose x[sender] / w rows are loaded together
+      one iteration ahead (sender indices two iterations ahead): two edges' loads in flight
+      per wave at every wait instead of one (the copy of the prefetched registers at the end
+      of an iteration is where the wave waits for them).
+    The receiver-segmented sum, flush and XCD placement are tp_fwd's.  Every iteration but a
+    stream's last consumes the same number of edges in both half-waves, so the batch boundary
+    is uniform across the wave."""
+    B = TP_M_B
+    PAIR = TP_M_PAIR
+    assert B >= 2 and B & (B - 1) == 0
+    ng = len(groups)
+    gents = [_group_entries(g) for g in groups]
+    maxch = max((len(e) + 3) // 4 for e in gents)
+    slab = maxch * B + 1                       # float4s per half-wave (+1: bank offset between halves)
+    L: List[str] = []
+    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append(f"  __shared__ float4 mbuf[8 * {slab}];")
+    L.append("  const int lane = threadIdx.x & 63;")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append(f"  const int slot = lane & {B - 1};")
+    L.append(f"  const bool writer = (lane & 31) < {B};")
+    L.append(f"  float4* __restrict__ mb = mbuf + (threadIdx.x >> 5) * {slab};")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    if TP_XCD_CONTIG:
+        # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the
+        # x rows of a lattice are gathered by one XCD (its L2) rather than by all eight
+        L.append(f"  const int ntl = (n_nodes + {8 * TP_NPH - 1}) / {8 * TP_NPH}, tpx = (ntl + 7) >> 3;")
+        L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    else:
+        L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
+    L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
+    L.append("  if (n0 >= n_nodes) return;")
+    L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
+    L.append("  switch (grp) {")
+    only = os.environ.get("EELG_TP_M_ONLY")            # register-budget probe: one group only
+    for gi, (grp, ents) in enumerate(zip(groups, gents)):
+        if only is not None and gi != int(only):
+            continue
+        L.append(f"  case {gi}: {{")
+        need_l1 = sorted({p.l1 for p in grp})
+        need_j = sorted({j for *_, ts in ents for _, j in ts})
+        need_l2 = sorted({l for l in range(9) for j in need_j if l * l <= j < (l + 1) * (l + 1)})
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        xw_ = [f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)] + [f"w{p.slot}" for p in grp]
+        ys_ = [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+        nch = (len(ents) + 3) // 4
+        sets = ["c0_", "c1_"] if PAIR else ["c0_"]        # register sets in use (one per edge)
+        nsets = ["n0_", "n1_"] if PAIR else ["n0_"]       # their prefetch
+        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
+        L.append("    int e = rowptr[n0];")
+        L.append("    const int eend = rowptr[n1];")
+        L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
+        L.append("    float " + ", ".join(pf + v for pf in sets for v in xw_) + ", " + ", ".join(ys_) + ";")
+
+        def ld_xw(pref, ev, sv, ind="    "):
+            """x[sender] slices and the group's weights of edge ``ev`` (clamped addresses when
+            the edge does not exist: the values are then never used)"""
+            out = [f"{ind}{{ const bool ok = {ev} < eend;",
+                   f"{ind}  const float* __restrict__ xs = x + (size_t)(ok ? {sv} : 0) * {din};",
+                   f"{ind}  const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
+            for l in need_l1:
+                d = 2 * l + 1
+                out += [f"{ind}  " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
+                                                          f"{node_off[l]} + u * {d}")]
+            for p in grp:
+                out.append(f"{ind}  {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
+            out.append(f"{ind}}}")
+            return out
+
+        def ld_y(ev, ind="    "):
+            """this lane's SH row of edge ``ev`` straight into the y registers (clamped; rows
+            past the stream are unused); consumed by the next phase 1, a batch later"""
+            out = [f"{ind}{{ const float* __restrict__ ye = sh + (size_t)min({ev}, max(eend - 1, 0)) * {nshp};"]
+            out += [f"{ind}  " + ln for ln in sh_load(need_l2, "", "ye")]
+            out.append(f"{ind}}}")
+            return out
+
+        def flush(ind):
+            out = [f"{ind}while (node < n1 && nend == e) {{",
+                   f"{ind}  float* __restrict__ o = agg + (size_t)node * {dmid};"]
+            for p in grp:
+                d3 = 2 * p.l3 + 1
+                out.extend(f"{ind}  " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                              f"{p.out_off} + u * {d3}"))
+            out.append(f"{ind}  " + " ".join(f"{a} = 0.0f;" for a in accs))
+            out.append(f"{ind}  ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
+            out.append(f"{ind}}}")
+            return out
+
+        # phase 2 consumes the entries in order; chunk c + TP_M_AHEAD is read when chunk c is
+        # first used, and a pin with a memory clobber after each chunk keeps the reads there
+        # (the compiler would otherwise hoist every chunk read: registers)
+        AH = TP_M_AHEAD
+
+        def compute(cp, es, ind):
+            out = [f"{ind}{{"]
+            loaded = set()
+            state = {"cur": -1}
+            pn = pin(accs + [pf + v for pf in sets for v in xw_], memory=True)
+
+            def need(t):
+                c = t // 4
+                if c != state["cur"]:
+                    if state["cur"] >= 0:
+                        out.append(f"{ind}" + pn)
+                    for cc in range(c, min(c + AH + 1, nch)):
+                        if cc not in loaded:
+                            loaded.add(cc)
+                            out.append(f"{ind}const float4 mc{cc} = mb[{cc * B} + {es}];")
+                    state["cur"] = c
+                return f"mc{c}.{'xyzw'[t % 4]}"
+            t = 0
+            for p in grp:
+                d1, d3 = 2 * p.l1 + 1, 2 * p.l3 + 1
+                pents = [e_ for e_ in ents if e_[0] is p]
+                out.append(f"{ind}// slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}, {len(pents)} coupling entries")
+                if d1 <= d3:
+                    for i in range(d1):
+                        out.append(f"{ind}const float xw{p.slot}_{i} = {cp}x{p.l1}_{i} * {cp}w{p.slot};")
+                    for e_ in pents:
+                        _, i, k, _ = e_
+                        m = need(t)
+                        out.append(f"{ind}a{p.slot}_{k} = fmaf({m}, xw{p.slot}_{i}, a{p.slot}_{k});")
+                        t += 1
+                else:
+                    n = 0
+                    while n < len(pents):
+                        k = pents[n][2]
+                        run = []
+                        while n < len(pents) and pents[n][2] == k:
+                            run.append(pents[n])
+                            n += 1
+                        m = need(t)
+                        out.append(f"{ind}float t{p.slot}_{k} = {m} * {cp}x{p.l1}_{run[0][1]};")
+                        t += 1
+                        for e_ in run[1:]:
+                            m = need(t)
+                            out.append(f"{ind}t{p.slot}_{k} = fmaf({m}, {cp}x{p.l1}_{e_[1]}, t{p.slot}_{k});")
+                            t += 1
+                        out.append(f"{ind}a{p.slot}_{k} = fmaf({cp}w{p.slot}, t{p.slot}_{k}, a{p.slot}_{k});")
+            out.append(f"{ind}" + pn)
+            out.append(f"{ind}}}")
+            return out
+
+        # prologue: this batch's SH rows, the first edges' operands, sender indices ahead
+        L += ld_y("e + slot")
+        for k, pf in enumerate(sets):
+            L += ld_xw(pf, f"e + {k}", f"sender[e + {k}]")
+        nxt = len(sets)
+        L.append("    " + " ".join(f"int s{k} = sender[min(e + {nxt + k}, max(eend - 1, 0))];"
+                                   for k in range(len(sets))))
+        L.append("    const int ebase = e;")
+        L.append("    for (;;) {")
+        L.append("      float " + ", ".join(pf + v for pf in nsets for v in xw_) + ";")
+        L += flush("      ")
+        L.append("      if (e >= eend) break;")
+        # ---- phase 1 at a batch boundary: M of edges e .. e+B-1 into the slab ----
+        L.append(f"      if (((e - ebase) & {B - 1}) == 0) {{")
+        L.append("        " + " ".join(f"y{j} *= inv_norm;" for j in need_j))
+        for c in range(nch):
+            vals = []
+            for t in range(4 * c, 4 * c + 4):
+                if t >= len(ents):
+                    vals.append("0.0f")
+                    continue
+                _, _, _, ts = ents[t]
+                ex = f"{flit(ts[0][0])} * y{ts[0][1]}"
+                for cc, j in ts[1:]:
+                    ex = f"fmaf({flit(cc)}, y{j}, {ex})"
+                vals.append(ex)
+            L.append(f"        {{ const float4 m_ = make_float4({', '.join(vals)});")
+            L.append(f"          if (writer) mb[{c * B} + slot] = m_; }}")
+            # each chunk is computed and stored in place (not hoisted: registers)
+            L.append("        " + pin([f"y{j}" for j in need_j], memory=True))
+        L.append("        __builtin_amdgcn_wave_barrier();")
+        L += ld_y(f"e + {B} + slot", "        ")
+        L.append("      }")
+        # ---- prefetch the next iteration's edges; sender indices one more iteration ahead ----
+        L.append("      { " + " ".join(f"const int t{k} = sender[min(e + {2 * nxt + k}, eend - 1)];"
+                                       for k in range(len(sets))))
+        for k, pf in enumerate(nsets):
+            L += ld_xw(pf, f"e + {nxt + k}", f"s{k}", "      ")
+        L.append(f"      const int es = (e - ebase) & {B - 1};")
+        # ---- phase 2 ----
+        L += compute(sets[0], "es", "      ")
+        L.append("      ++e;")
+        if PAIR:
+            L += flush("      ")
+            L.append("      if (e < eend) {")
+            L += compute(sets[1], "es + 1", "        ")
+            L.append("        ++e;")
+            L.append("      }")
+        L.append("      " + " ".join(f"{cs}{v} = {ns}{v};" for cs, ns in zip(sets, nsets) for v in xw_)
+                 + " " + " ".join(f"s{k} = t{k};" for k in range(len(sets))) + " }")
+        L.append("    }")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
+def _tp_path_cost(p: cg.TPPath) -> int:
+    """VALU instructions per lane of one path in the per-lane CG form (_emit_acc), plus its
+    operand reads: the balance weight of the cooperative forward's path partition."""
+    nz = _path_cg(p)
+    pairs = len({(i, j) for (i, j, k), _ in nz})
+    iks = len({(i, k) for (i, j, k), _ in nz})
+    d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
+    return min(d3 + 1, d1, d2) + (pairs + len(nz) if pairs <= iks else len(nz) + iks) + 2
+
+
+def coop_groups(paths: List[cg.TPPath], ng: int, max_acc: int) -> List[List[cg.TPPath]]:
+    """Partition the paths into ``ng`` groups of balanced VALU cost (longest-processing-time
+    greedy) with at most ``max_acc`` accumulators per lane each; within a group the paths are
+    in (l1, l2, l3) order.  All groups of the cooperative forward meet at every batch barrier,
+    so the slowest group sets the pace."""
+    bins = [[0, 0, []] for _ in range(ng)]
+    for p in sorted(paths, key=lambda p: (-_tp_path_cost(p), p.slot)):
+        cand = [b for b in bins if b[1] + 2 * p.l3 + 1 <= max_acc]
+        if not cand:
+            raise ValueError(f"cannot place path {p} under {max_acc} accumulators in {ng} groups")
+        b = min(cand, key=lambda b: (b[0], b[1]))
+        b[0] += _tp_path_cost(p)
+        b[1] += 2 * p.l3 + 1
+        b[2].append(p)
+    return [sorted(b[2], key=lambda p: (p.l1, p.l2, p.l3)) for b in bins if b[2]]
+
+
+def tp_coop_shape(paths: List[cg.TPPath]) -> int:
+    """Waves (= path groups) per block of the cooperative forward."""
+    n = len(paths)
+    return 8 if n >= 32 else 4 if n >= 12 else 2 if n >= 4 else 1
+
+
+def emit_tp_fwd_coop(name, sfx, WT, ld_w, paths, din, nshp, wn, dmid, node_off, bf) -> Tuple[List[str], dict]:
+    """Cooperative forward: one block = NG waves = NG balanced path groups, over two receiver
+    tiles (lanes 0-31 of every wave on tile A, lanes 32-63 on tile B: the two halves of a wave
+    run the same group's code on different receivers).
+
+    The tiles' edges are staged in batches of TP_CO_BE edges per tile: for each edge the whole
+    x[sender] row, the whole TP-weight row and the SH row are copied once into LDS by all the
+    block's threads (float4 loads, issued a batch ahead into registers and written after the
+    batch barrier), and every group wave reads its operands from there.  Against one block per
+    path group (tp_fwd_m / the per-group kernel) each edge's rows cross L2 once instead of once
+    per group, the weight rows stream contiguously, and the receivers' output rows are written
+    by all groups at the same time (whole-row write locality).  Sender indices of a batch are
+    staged in LDS one batch earlier still, so staging has no dependent global-load chain."""
+    NG = tp_coop_shape(paths)
+    groups = coop_groups(paths, NG, TP_CO_MAXACC)
+    NG = len(groups)
+    NT = 64 * NG
+    BE = TP_CO_BE
+    R = TP_CO_R
+    es = 2 if bf else 4
+    X4, W4, Y4 = din // 4, wn * es // 16, nshp // 4
+    assert din % 4 == 0 and (wn * es) % 16 == 0 and nshp % 4 == 0
+    ROW4 = X4 + W4 + Y4
+    if ROW4 % 2 == 0:
+        ROW4 += 1                         # odd row stride: the two tiles' rows start in other banks
+    SLOTS = 2 * BE * ROW4
+    # staging work: per kind (x rows, weight rows, SH rows) a compile-time run of float4 slots,
+    # so every load's source kind is static (no per-slot branches or pointer selects)
+    kinds = [("x", X4, 0), ("w", W4, X4), ("y", Y4, X4 + W4)]
+    plan = []                                  # (kind, i): slot j = tid + NT * i of that kind
+    for kd, n4, off in kinds:
+        tot = 2 * BE * n4
+        for i in range((tot + NT - 1) // NT):
+            plan.append((kd, n4, off, i, tot))
+    NS = len(plan)
+    L: List[str] = []
+    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_CO_WPE})))" if TP_CO_WPE else ""
+    L.append(f"__global__ __launch_bounds__({NT}){wpe} void tp_fwd_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append(f"  __shared__ float4 st[{SLOTS}];")
+    L.append(f"  __shared__ int sidx[{2 * BE}];")
+    L.append("  const int tid = threadIdx.x, lane = tid & 63, u = lane & 31, h = lane >> 5;")
+    # XCD-aware: the blocks of XCD k (blockIdx % 8 == k) take one contiguous range of tile pairs
+    L.append(f"  const int nb = (n_nodes + {2 * R - 1}) / {2 * R}, nb8 = (nb + 7) >> 3;")
+    L.append("  const int b = (blockIdx.x & 7) * nb8 + (blockIdx.x >> 3);")
+    L.append("  if (b >= nb) return;")
+    L.append(f"  const int rA = min(2 * b * {R}, n_nodes), rB = min(rA + {R}, n_nodes), rC = min(rB + {R}, n_nodes);")
+    L.append("  const int eA = rowptr[rA], eB = rowptr[rB], eC = rowptr[rC];")
+    L.append("  const int r0 = h ? rB : rA, r1 = h ? rC : rB, e0 = h ? eB : eA, e1 = h ? eC : eB;")
+    L.append(f"  const int nbatch = (max(eB - eA, eC - eB) + {BE - 1}) / {BE};")
+    L.append("  float4 " + ", ".join(f"sr{i}" for i in range(NS)) + ";")
+    L.append("  int snext = 0;")
+
+    def issue(bexpr, ind):
+        """loads of batch ``bexpr`` (its sender indices already in sidx) into sr; sender indices
+        of batch bexpr + 1 into snext"""
+        # tid made opaque here: the per-slot index math is recomputed per batch (a few integer
+        # ops) instead of being hoisted out of the batch loop into registers
+        out = [f"{ind}{{ const int bb = {bexpr}; int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));"]
+        out.append(f"{ind}  if (tid < {2 * BE}) {{ const int hh = tid / {BE}, k = tid - hh * {BE};")
+        out.append(f"{ind}    const int e = (hh ? eB : eA) + (bb + 1) * {BE} + k, ee = hh ? eC : eB;")
+        out.append(f"{ind}    snext = sender[min(e, max(ee - 1, 0))]; }}")
+        for si, (kd, n4, off, i, tot) in enumerate(plan):
+            out.append(f"{ind}  {{ const int j = min(tid + {NT * i}, {tot - 1});")
+            out.append(f"{ind}    const int hk = j / {n4}, f = j - hk * {n4}, hh = hk / {BE}, k = hk - hh * {BE};")
+            if kd == "x":
+                out.append(f"{ind}    sr{si} = reinterpret_cast<const float4*>(x + (size_t)sidx[hk] * {din})[f]; }}")
+            else:
+                out.append(f"{ind}    const int e = min((hh ? eB : eA) + bb * {BE} + k, max((hh ? eC : eB) - 1, 0));")
+                if kd == "w":
+                    out.append(f"{ind}    sr{si} = reinterpret_cast<const float4*>(w + (size_t)e * {wn})[f]; }}")
+                else:
+                    out.append(f"{ind}    sr{si} = reinterpret_cast<const float4*>(sh + (size_t)e * {nshp})[f]; }}")
+        out.append(f"{ind}}}")
+        return out
+
+    def commit(ind):
+        out = [f"{ind}{{ int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));"]
+        for si, (kd, n4, off, i, tot) in enumerate(plan):
+            guard = f"tid + {NT * i} < {tot}" if NT * (i + 1) > tot else "true"
+            out.append(f"{ind}{{ const int j = tid + {NT * i}; if ({guard}) {{ const int hk = j / {n4}; "
+                       f"st[hk * {ROW4} + {off} + (j - hk * {n4})] = sr{si}; }} }}")
+        out.append(f"{ind}if (tid < {2 * BE}) sidx[tid] = snext; }}")
+        return out
+
+    # prologue: sender indices of batch 0, then batch 0's rows (and batch 1's indices)
+    L.append(f"  if (tid < {2 * BE}) {{ const int hh = tid / {BE}, k = tid - hh * {BE};")
+    L.append(f"    const int e = (hh ? eB : eA) + k, ee = hh ? eC : eB;")
+    L.append(f"    sidx[tid] = sender[min(e, max(ee - 1, 0))]; }}")
+    L.append("  __syncthreads();")
+    L += issue("0", "  ")
+    L.append("  __syncthreads();")
+    L += commit("  ")
+    L.append("  __syncthreads();")
+    L.append(f"  switch (tid >> 6) {{")
+    only = os.environ.get("EELG_TP_CO_ONLY")           # register-budget probe: one group only
+    for gi, grp in enumerate(groups):
+        if only is not None and gi != int(only):
+            continue
+        need_l1 = sorted({p.l1 for p in grp})
+        need_l2 = sorted({p.l2 for p in grp})
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        L.append(f"  case {gi}: {{ // {len(grp)} paths, {len(accs)} accumulators, cost {sum(_tp_path_cost(p) for p in grp)}")
+        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
+        L.append("    int e = e0, node = r0;")
+        L.append("    int nend = r0 < r1 ? rowptr[r0 + 1] : e1, nend2 = rowptr[min(r0 + 2, r1)];")
+
+        def flush(ind):
+            out = [f"{ind}while (node < r1 && nend == e) {{",
+                   f"{ind}  float* __restrict__ o = agg + (size_t)node * {dmid};"]
+            for p in grp:
+                d3 = 2 * p.l3 + 1
+                out.extend(f"{ind}  " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                              f"{p.out_off} + u * {d3}"))
+            out.append(f"{ind}  " + " ".join(f"{a} = 0.0f;" for a in accs))
+            out.append(f"{ind}  ++node; nend = nend2; nend2 = rowptr[min(node + 2, r1)];")
+            out.append(f"{ind}}}")
+            return out
+        L.append("    for (int bi = 0; bi < nbatch; ++bi) {")
+        L += issue("bi + 1", "      ")
+        L.append(f"      const int kend = min({BE}, e1 - e);")
+        L.append("      for (int k = 0; k < kend; ++k) {")
+        L += flush("        ")
+        L.append(f"        const float4* __restrict__ rw = st + (h * {BE} + k) * {ROW4};")
+        L.append("        const float* __restrict__ xs = reinterpret_cast<const float*>(rw);")
+        L.append(f"        const {WT}* __restrict__ we = reinterpret_cast<const {WT}*>(rw + {X4}) + u;")
+        L.append(f"        const float* __restrict__ ye = reinterpret_cast<const float*>(rw + {X4 + W4});")
+        # operands are read from LDS per path (short live ranges: registers), the pins after
+        # each path keep the reads there
+        xn = lambda p, i: f"px{i}"  # noqa: E731
+        yn = lambda p, j: f"py{j}"  # noqa: E731
+        for p in grp:
+            d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
+            L.append(f"        {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append("          " + " ".join(f"const float px{i} = xs[{node_off[p.l1]} + u * {d1} + {i}];"
+                                             for i in range(d1)))
+            L.append("          float " + ", ".join(f"py{j}" for j in range(d2)) + ";")
+            L += ["          " + ln for ln in vec_load([f"py{j}" for j in range(d2)], "ye", str(p.l2 * p.l2))]
+            L.append(f"          const float wp = {ld_w(f'we[{p.slot * MUL}]')} * ({flit(p.coef)} * inv_norm);")
+            fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
+            if fold[1] == "none":
+                _emit_t(p, xn, yn, "t", L, "          ")
+                for k in range(d3):
+                    L.append(f"          a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+            else:
+                if fold[1] == "x":
+                    for i in range(d1):
+                        L.append(f"          const float xw{i} = {xn(p, i)} * wp;")
+                    xf, yf = (lambda p, i: f"xw{i}"), yn
+                else:
+                    for j in range(d2):
+                        L.append(f"          const float yw{j} = {yn(p, j)} * wp;")
+                    xf, yf = xn, (lambda p, j: f"yw{j}")
+                _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", L, "          ")
+            L.append("        }")
+            L.append("        " + pin(accs, memory=True))
+        L.append("        ++e;")
+        L.append("      }")
+        L.append("      __syncthreads();")
+        L += commit("      ")
+        L.append("      __syncthreads();")
+        L.append("    }")
+        L += flush("    ")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L, {"fwd_threads": NT, "fwd_tile": 2 * R, "ngroups": NG}
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -399,8 +883,16 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
+    coop = None
     if TP_PK2 and node_ls != [0]:
         L += emit_tp_fwd_pk2(name, sfx, WT, bf, groups, din, nshp, wn, dmid, node_off)
+        fwd_done = True
+    elif TP_COOP:
+        code, coop = emit_tp_fwd_coop(name, sfx, WT, ld_w, paths, din, nshp, wn, dmid, node_off, bf)
+        L += code
+        fwd_done = True
+    elif TP_FWD_M:
+        L += emit_tp_fwd_m(name, sfx, WT, ld_w, groups, din, nshp, nsh, wn, dmid, node_off)
         fwd_done = True
     else:
         fwd_done = False
@@ -412,7 +904,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
     L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-    L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
+    if TP_XCD_CONTIG:
+        # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the
+        # x rows of a lattice are gathered by one XCD (its L2) rather than by all eight
+        L.append(f"  const int ntl = (n_nodes + {8 * TP_NPH - 1}) / {8 * TP_NPH}, tpx = (ntl + 7) >> 3;")
+        L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    else:
+        L.append(f"  const int tile = (q / {ng}) * 8 + (blockIdx.x & 7);")
     L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
     L.append("  if (n0 >= n_nodes) return;")
     L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
@@ -473,7 +971,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             cpin_mid = pin(accs + [cp + v for v in cur]) if TP_PIN_NEXT_LAST else cpin
             xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
             yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
-            for p in grp:
+            if TP_NOCOMPUTE:
+                # diagnostic (memory-pattern floor): every loaded value feeds one sum that is
+                # added to every accumulator; the loads, stores and loop are tp_fwd's own
+                out.append("      { const float z_ = " + " + ".join(cp + v for v in cur) + ";")
+                out.append("        " + " ".join(f"{a} += z_;" for a in accs) + " }")
+                out.append("      " + cpin)
+            for p in ([] if TP_NOCOMPUTE else grp):
                 d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
                 out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
                 out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
@@ -722,7 +1226,10 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
                 npaths=len(paths), nph=2 * TP_NPH if pk2 else TP_NPH, beph=TP_BWD_EPH,
-                sig=fnv1a64(tp_signature(node, sh, target)))
+                sig=fnv1a64(tp_signature(node, sh, target)),
+                fwd_threads=coop["fwd_threads"] if coop else 256, fwd_tile=coop["fwd_tile"] if coop else 0)
+    if coop:
+        info["ngroups"] = coop["ngroups"]
     return "\n".join(L), info
 
 
@@ -1364,7 +1871,8 @@ def main(outdir: str) -> None:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                      f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
+                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw, '
+                     f'{i["fwd_threads"]}, {i["fwd_tile"]}}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:
