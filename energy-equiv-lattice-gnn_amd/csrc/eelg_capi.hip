@@ -647,7 +647,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3(mul / (c->fwd_cp ? 8 : 4), (n_nodes + (c->fwd_cp ? 64 : c->nb) - 1) / (c->fwd_cp ? 64 : c->nb)), dim3(256), 0,
+  hipLaunchKernelGGL(c->fwd, dim3(mul / (c->fwd_cp ? 8 : 4), (n_nodes + (c->fwd_cp ? 64 : c->nb) - 1) / (c->fwd_cp ? 64 : c->nb)), dim3(c->fwd_cp ? 256 : c->nth), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -662,7 +662,7 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(c->nth), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
 }

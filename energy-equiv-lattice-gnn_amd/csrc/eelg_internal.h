@@ -55,6 +55,7 @@ struct eelg_sc_cfg {
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
   int coef_mm;                   // 1: coef-grad reads mul-major x / grad_out (1-D XCD-grouped grid)
   int fwd_cp;                    // 1: sc_fwd holds two channels per lane, coefficients channel-pair interleaved
+  int nth;                       // threads per fwd / grad-x workgroup
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -35,7 +35,7 @@ from gnn.irreps import Ir, Irreps  # noqa: E402
 MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
-TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "32"))
+TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 TP_NOPIN_NEXT = int(os.environ.get("EELG_TP_NOPIN_NEXT", "0"))
 TP_PIN_NEXT_LAST = int(os.environ.get("EELG_TP_PIN_NEXT_LAST", "1"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
@@ -57,6 +57,9 @@ SC_CP_MAXB = int(os.environ.get("EELG_SC_CP_MAXB", "16"))
 # computed, forward / grad-x (r02: grad-x 0.56 -> 0.51 ms at 3; the forward spills SGPRs at 2+)
 SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
 SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "3"))
+# symmetric contraction fwd / grad-x: 64-node tiles per workgroup (2: waves of one channel share
+# its coefficient stream through the scalar cache; measured slower r03h: fwd 0.40 vs 0.37 ms)
+SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, sub-tile unroll
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
 SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
@@ -1364,7 +1367,12 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     # nodes per lane in plain fp32 (a two-float struct: every coefficient scalar load and LDS
     # coefficient fetch feeds two independent FMAs, no packed-operand constraints)
     PKN = 2 if SC_PK in (2, 3) else 1
-    NB = 64 * PKN                           # nodes per workgroup (fwd / grad-x)
+    # node tiles per workgroup (fwd / grad-x): waves w and w + 4 run the same channel on two
+    # 64-node tiles, so the second wave's coefficient scalar loads hit the scalar cache line
+    # the first one brought in
+    NT = SC_NT if PKN == 1 else 1
+    NB = 64 * PKN * NT                      # nodes per workgroup (fwd / grad-x)
+    NTH = 256 * NT                          # threads per workgroup
     FT = {1: "float", 2: "eelg_f2", 3: "eelg_d2"}[SC_PK]
     ZERO = "0.0f" if PKN == 1 else f"{FT}{{0.0f, 0.0f}}"
 
@@ -1385,30 +1393,30 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
             return f"{base0}[{col}] = {val};"
         return f"{base0}[{col}] = {val}.x; {base1}[{col}] = {val}.y;"
 
-    def stage_in(src, tile, lay, nb=64):
-        per = (nb * lay.QD + 255) // 256
+    def stage_in(src, tile, lay, nb=64, nth=256):
+        per = (nb * lay.QD + nth - 1) // nth
         out = ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                "#pragma unroll 2",
                f"  for (int it = 0; it < {per}; ++it) {{",
-               f"    const int idx = tid + 256 * it;",
+               f"    const int idx = tid + {nth} * it;",
                f"    if (idx < {nb * lay.QD}) {{",
                f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
                f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] : 0.0f;",
                "    }", "  } }"]
         return out
 
-    def stage_out(dst, tile, lay, nb=64):
-        per = (nb * lay.QD + 255) // 256
+    def stage_out(dst, tile, lay, nb=64, nth=256):
+        per = (nb * lay.QD + nth - 1) // nth
         return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
                 "#pragma unroll 2",
                 f"  for (int it = 0; it < {per}; ++it) {{",
-                f"    const int idx = tid + 256 * it;",
+                f"    const int idx = tid + {nth} * it;",
                 f"    if (idx < {nb * lay.QD}) {{",
                 f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
                 f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = {tile}[nl * {TP} + q];",
                 "    }", "  } }"]
 
-    def cm_store(dst, tile, lay, nb, ind="  "):
+    def cm_store(dst, tile, lay, nb, ind="  ", nth=256):
         """dst[(c * D + a) * n_nodes + n] = component a of channel c of node n, from a staged
         tile of nb nodes x the quad's 4 channels (coalesced nb-float runs per (c, a))"""
         dd = lay.D
@@ -1416,10 +1424,10 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
         dls = ", ".join(str(2 * lay.comp[a][0] + 1) for a in range(dd))
         ms = ", ".join(str(lay.comp[a][1]) for a in range(dd))
         sh = nb.bit_length() - 1
-        per = (Q * dd * nb + 255) // 256
+        per = (Q * dd * nb + nth - 1) // nth
         out = [f"{{ const int kseg[{dd}] = {{{sgs}}}, kd[{dd}] = {{{dls}}}, km[{dd}] = {{{ms}}};",
                f"  for (int it = 0; it < {per}; ++it) {{",
-               "    const int idx = threadIdx.x + 256 * it;",
+               f"    const int idx = threadIdx.x + {nth} * it;",
                f"    if (idx < {Q * dd * nb}) {{",
                f"      const int row = idx >> {sh}, nl = idx & {nb - 1}, n = n0 + nl;",
                f"      const int cl = row / {dd}, a = row - cl * {dd};",
@@ -1443,21 +1451,22 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
 
     head = ["  const int cq = blockIdx.x;", f"  const int n0 = blockIdx.y * {NB};",
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
-            f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + wv);",
-            f"  const int cl = __builtin_amdgcn_readfirstlane(wv);",
+            f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
+            f"  const int cl = __builtin_amdgcn_readfirstlane(wv & {Q - 1});",
+            f"  const int nrow = (wv >> 2) * 64 + lane;      // this lane's node row in the tile",
             f"  const float* __restrict__ cf = coef + (size_t)c * {nt};"]
 
     # ---------------- forward ----------------
     if not SC_FWD_CP:
-        L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
+        L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
         L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
         L.append("    float* __restrict__ out) {")
         L.append(f"  __shared__ float tile[{NB} * {TP}];")
         L += head
-        L += stage_in("x", "tile", lin, NB)
+        L += stage_in("x", "tile", lin, NB, NTH)
         L.append("  __syncthreads();")
         # packed: a lane owns nodes n0 + lane and n0 + 64 + lane (one v_pk_* op covers both)
-        L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
+        L.append(f"  float* __restrict__ tr = tile + nrow * {TP};")
         if PKN == 2:
             L.append(f"  float* __restrict__ tr1 = tile + (lane + 64) * {TP};")
         for a in range(D):
@@ -1497,7 +1506,7 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
         for q in range(Dout):
             L.append("  " + st_pair(f"o{q}", "tr", "tr1", lq(lout, q, 'cl')))
         L.append("  __syncthreads();")
-        L += stage_out("out", "tile", lout, NB)
+        L += stage_out("out", "tile", lout, NB, NTH)
         L.append("}")
 
     else:
@@ -1600,7 +1609,7 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
         L.append("}")
 
     # ---------------- backward w.r.t. x ----------------
-    L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
     L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
@@ -1609,22 +1618,22 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
     L.append(f"  __shared__ float tx[{NB} * {TP}];")
     L += head
-    L += stage_in("x", "tx", lin, NB)
+    L += stage_in("x", "tx", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (xt) {")
-    L += cm_store("xt", "tx", lin, NB, "    ")
+    L += cm_store("xt", "tx", lin, NB, "    ", NTH)
     L.append("  }")
-    L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
+    L.append(f"  float* __restrict__ xr = tx + nrow * {TP};")
     if PKN == 2:
         L.append(f"  float* __restrict__ xr1 = tx + (lane + 64) * {TP};")
     for a in range(D):
         L.append("  " + ld_pair(f"x{a}", "xr", "xr1", lq(lin, a, 'cl')))
         L.append(f"  {FT} d{a} = {ZERO};")
     L.append("  __syncthreads();")
-    L += stage_in("gout", "tx", lout, NB)
+    L += stage_in("gout", "tx", lout, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (gt) {")
-    L += cm_store("gt", "tx", lout, NB, "    ")
+    L += cm_store("gt", "tx", lout, NB, "    ", NTH)
     L.append("  }")
     for q in range(Dout):
         L.append("  " + ld_pair(f"g{q}", "xr", "xr1", lq(lout, q, 'cl')))
@@ -1662,7 +1671,7 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     for a in range(D):
         L.append("  " + st_pair(f"d{a}", "xr", "xr1", lq(lin, a, 'cl')))
     L.append("  __syncthreads();")
-    L += stage_out("gx", "tx", lin, NB)
+    L += stage_out("gx", "tx", lin, NB, NTH)
     L.append("}")
 
     # ---------------- mul-major -> channel-major transpose ----------------
@@ -1823,7 +1832,7 @@ def _emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC, nth=NTH,
                 coef_mulmajor=SC_COEF_MULMAJOR, fwd_cp=SC_FWD_CP,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
@@ -1878,7 +1887,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}, {i["coef_mulmajor"]}, {i["fwd_cp"]}}},')
+                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}, {i["coef_mulmajor"]}, {i["fwd_cp"]}, {i["nth"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -2,7 +2,7 @@
 
 CPU: the oracle reproduces the committed outputs (pins the oracle against drift).
 GPU: the HIP path reproduces them within the fp32 tolerance stated in
-test_gpu_parity.py (stiffness 1e-4 relative to max|C|, loss 1e-4, grads 1e-3)."""
+test_gpu_parity.py (stiffness 1e-4 relative to max|C|, loss 1e-4, grads 2e-5)."""
 import os
 
 import numpy as np
@@ -78,5 +78,10 @@ def test_hip_path_reproduces_golden():
     assert rel(c, g["out_stiffness"]) < 1e-4
     assert abs(loss.item() - float(g["out_loss"])) < 1e-4 * abs(float(g["out_loss"]))
     grads = dict(m.named_parameters())
+    # every parameter gradient within 2e-5 of its own largest entry (fp32 HIP vs the fp64
+    # golden: reduction-order noise; the model parity tests measure <= 2.3e-6)
+    worst = max(rel(grads[k].grad, g["grad/" + k]) for k in [k[5:] for k in g if k.startswith("grad/")])
+    from helpers import record_parity
+    record_parity("golden_config1", stiffness=rel(c, g["out_stiffness"]), grad_params=worst)
     for k in [k[5:] for k in g if k.startswith("grad/")]:
-        assert rel(grads[k].grad, g["grad/" + k]) < 1e-3, k
+        assert rel(grads[k].grad, g["grad/" + k]) < 2e-5, k

@@ -16,7 +16,7 @@ import torch
 import oracle.model as omodel
 from oracle.train import stiffness_loss as oracle_loss
 
-from helpers import batch_to, copy_params, params
+from helpers import batch_to, copy_params, params, record_parity
 from helpers_mandel import rotate_mandel
 
 pytestmark = pytest.mark.gpu
@@ -86,7 +86,9 @@ def test_fullsize_gradient_is_sum_over_graphs(full):
     gb = grads(bd)
     gs = sum(grads(collate([ds[gi]]).to(DEV)) for gi in range(4))
     gb4 = grads(collate([ds[gi] for gi in range(4)]).to(DEV))
-    assert rel_err(gb4, gs) < 1e-3
+    # fp32 on both sides, only the summation order over graphs differs
+    record_parity("fullsize_grad_sum_over_graphs", grad=rel_err(gb4, gs))
+    assert rel_err(gb4, gs) < 2e-5
     assert torch.isfinite(gb).all()
 
 
@@ -133,9 +135,11 @@ def test_edge_cases_vs_oracle():
     b = collate(graphs)
     rmax = float(b.edge_attr.max())
     err, gerr = _oracle_pair(b, rmax)
-    assert err < 1e-4, err
-    assert gerr < 1e-3, gerr
-    # a single graph, single edge pair
+    # gradients within 2e-5 of each parameter's largest entry (the in-degree-300 hub sums 300
+    # per-edge terms per channel: reduction-order noise only)
     b1 = collate([_graph(2, [(0, 1), (1, 0)], seed=9)])
     err1, gerr1 = _oracle_pair(b1, float(b1.edge_attr.max()))
-    assert err1 < 1e-4 and gerr1 < 1e-3
+    record_parity("edge_cases", stiffness=err, grad_params=gerr, single_pair=err1, single_pair_grad=gerr1)
+    assert err < 1e-4, err
+    assert gerr < 2e-5, gerr
+    assert err1 < 1e-4 and gerr1 < 2e-5

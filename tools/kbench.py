@@ -179,6 +179,15 @@ def main():
         rec(f"{name} bwd_w", timeit_if(f"{name} bwd_w", lambda: lin._bwd_w(xi, gy), args.reps), byt, fl)
     mlp = blk.conv_tp_weights
     ef = torch.randn(e, 12, device=dev, requires_grad=True)
+    efn = ef.detach()
+    rad_fl = 2 * e * (12 * 64 + 64 * 64 + 64 * info["wn"])
+    rec("radial fwd (HIP)", timeit_if("radial fwd (HIP)", lambda: ops.radial_mlp(efn, mlp), args.reps),
+        None, rad_fl)
+
+    def radfb():
+        out = ops.radial_mlp(efn, mlp)
+        out.backward(torch.ones_like(out))
+    rec("radial fwd+bwd (HIP)", timeit_if("radial fwd+bwd (HIP)", radfb, args.reps), None, 3 * rad_fl)
     rec("radial MLP fwd (torch)", timeit_if("radial MLP fwd (torch)", lambda: mlp(ef), args.reps), None,
         2 * e * (12 * 64 + 64 * 64 + 64 * info["wn"]))
 

@@ -21,6 +21,19 @@ with tempfile.TemporaryDirectory() as d:
         i = start
         while not src[i].startswith("__global__"):
             i -= 1
+        # the config section's device helpers (e.g. sc_goff_*) precede its first kernel
+        k = i
+        while k > 0 and not src[k].startswith("// ====="):
+            k -= 1
+        helpers, inside = [], False
+        for ln in src[k:i]:
+            if ln.startswith("__device__"):
+                inside = True
+            if inside:
+                helpers.append(ln)
+            if inside and ln.startswith("}"):
+                inside = False
+        body += [ln for ln in helpers if ln not in body]
         j = start + 1
         while j < len(src) and not src[j].startswith("__global__") and not src[j].startswith("// ====="):
             j += 1
