@@ -408,7 +408,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
-  info[5] = c.Dout; info[6] = c.nbc; info[7] = c.coef_mm; info[8] = c.fwd_cp;
+  info[5] = c.Dout; info[6] = c.nbc;
   *sig = c.sig;
   return 0;
 }
@@ -436,14 +436,9 @@ static const eelg_tp_cfg* tp_cfg(int cfg) {
 }
 
 // node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up to a
-// multiple of 8 so every tile's ngroups blocks land on one XCD (see gen_kernels.py)
-// cooperative forward (fwd_tile > 0): one block per fwd_tile receivers, the block count rounded
-// up to a multiple of 8 (XCD k takes a contiguous range of tiles; surplus blocks exit)
+// multiple of 8 so every tile's ngroups blocks land on one XCD, which takes a contiguous range
+// of tiles (see gen_kernels.py); surplus blocks exit
 static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes) {
-  if (c.fwd_tile > 0) {
-    const int nb = (n_nodes + c.fwd_tile - 1) / c.fwd_tile;
-    return dim3(((nb + 7) / 8) * 8);
-  }
   const int tiles = (n_nodes + 8 * c.nph - 1) / (8 * c.nph);
   return dim3(((tiles + 7) / 8) * 8 * c.ngroups);
 }
@@ -453,7 +448,7 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(c->fwd_threads), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x,
                      sh, w, sender, rowptr, n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");
 }
@@ -463,7 +458,7 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(c->fwd_threads), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream,
                      x, sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
                      agg);
   return check_launch("tp_fwd_bf16");
@@ -647,7 +642,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3(mul / (c->fwd_cp ? 8 : 4), (n_nodes + (c->fwd_cp ? 64 : c->nb) - 1) / (c->fwd_cp ? 64 : c->nb)), dim3(c->fwd_cp ? 256 : c->nth), 0,
+  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -662,7 +657,7 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(c->nth), 0,
+  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
 }
@@ -686,11 +681,9 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
     return fail(-2, "sc_bwd_coef: chunk must be the config's coefficient chunk %d (info[6]), got %d",
                 c->nbc, chunk);
   if (n_nodes <= 0) return 0;
-  // one workgroup per (chunk of nbc LDS-resident nodes, channel); mul-major operands: 1-D grid
-  // with the mul channel workgroups of a chunk back to back on one XCD
+  // one workgroup per (chunk of nbc LDS-resident nodes, channel)
   const int nch = (n_nodes + chunk - 1) / chunk;
-  const dim3 grid = c->coef_mm ? dim3(((nch + 7) / 8) * 8 * mul) : dim3(nch, mul);
-  hipLaunchKernelGGL(c->bwd_coef, grid, dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,
+  hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul), dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,
                      n_nodes, chunk, partial);
   return check_launch("sc_bwd_coef");
 }
@@ -717,42 +710,13 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
       const int g = (n_nodes + nb - 1) / nb;
       max_groups = g > max_groups ? g : max_groups;
     }
-    const int gpw = lin_jl_gpw();
-    if (gpw > 0 && lin_fwd_jl_ok(desc)) {
-      const int gbj = (max_groups + LINF_WAVES * gpw - 1) / (LINF_WAVES * gpw);
-      dim3 grid(((gbj + 7) / 8) * 8, desc->n_slots, 1);
-      hipLaunchKernelGGL(lin_fwd_fast_jl_kernel, grid, dim3(64 * LINF_WAVES), 0, (hipStream_t)stream,
-                         x, x_row, w, bias, n_nodes, y, y_row, *desc, res, gpw);
-      return check_launch("linear_fwd");
-    }
     const int gblocks = (max_groups + LINF_WAVES * LINF_GPW - 1) / (LINF_WAVES * LINF_GPW);
     dim3 grid(((gblocks + 7) / 8) * 8 * desc->max_jt, desc->n_slots, 1);
     int ws4;
     size_t lds;
     lin_fwd_fast_lds(desc, &ws4, &lds);
-    if (desc->max_jt == 1 && lin_bal_rounds() > 0) {
-      // balanced persistent form: one workgroup per resident slot (LDS- or VGPR-limited)
-      if (lds < lin_lds_floor()) lds = lin_lds_floor();
-      static bool bal_attr = false;
-      if (!bal_attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_bal_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-          return fail(-3, "linear_fwd: cannot raise the dynamic LDS limit");
-        bal_attr = true;
-      }
-      int per_cu = (int)((160 * 1024) / lds);
-      if (per_cu > LINF_BAL_MAXWG) per_cu = LINF_BAL_MAXWG;
-      if (per_cu < 1) per_cu = 1;
-      eelg_lin_bal_plan plan;
-      lin_bal_plan(desc, n_nodes, 256 * per_cu * lin_bal_rounds(), &plan);
-      hipLaunchKernelGGL(lin_fwd_bal_kernel, dim3(plan.wg_end[desc->n_slots - 1]), dim3(64 * LINF_WAVES),
-                         lds, (hipStream_t)stream, x, x_row, w, bias, n_nodes, y, y_row, *desc, res,
-                         ws4, plan);
-      return check_launch("linear_fwd");
-    }
     // one column tile per slot (the 800 -> 800 linears): two workgroups per CU measured faster
-    if (desc->max_jt == 1 && lds < lin_lds_1jt()) lds = lin_lds_1jt();
-    if (lds < lin_lds_floor()) lds = lin_lds_floor();
+    if (desc->max_jt == 1 && lds < LINF_LDS_1JT) lds = LINF_LDS_1JT;
     static bool lds_attr = false;   // > 64 KB of dynamic LDS must be allowed explicitly
     if (!lds_attr) {
       if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel),

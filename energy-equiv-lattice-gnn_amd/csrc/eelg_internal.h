@@ -38,8 +38,6 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_bf_fn bwd_bf;
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
-  int fwd_threads;           // tp_fwd block size
-  int fwd_tile;              // cooperative tp_fwd: receivers per block (0: one block per path group and node tile)
 };
 
 struct eelg_sc_cfg {
@@ -53,9 +51,6 @@ struct eelg_sc_cfg {
   eelg_sc_cmajor_fn cmajor_out;  // output layout
   int nb;                        // nodes per fwd / grad-x workgroup
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
-  int coef_mm;                   // 1: coef-grad reads mul-major x / grad_out (1-D XCD-grouped grid)
-  int fwd_cp;                    // 1: sc_fwd holds two channels per lane, coefficients channel-pair interleaved
-  int nth;                       // threads per fwd / grad-x workgroup
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -646,149 +646,6 @@ __device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ 
   }
 }
 
-// Column-tile loop variant (every slot's sources total one 32-wide K chunk, e.g. grad-x of the
-// 800 -> 7360 interaction linear: K = 32, up to 10 column tiles per slot).  A wave stages a
-// group's single K chunk once, keeps its 16 A operands in registers and runs every column tile
-// of the slot over them (weights of all tiles resident in LDS, row stride n_out), writing each
-// output tile through its LDS region: the input rows cross L2 once instead of once per tile.
-template <int D>
-__device__ __forceinline__ void lin_fwd_fast_jl(const float* __restrict__ x, int x_row,
-                                                const float* __restrict__ bias, int n_nodes,
-                                                float* __restrict__ y, int y_row,
-                                                const eelg_lin_slot& sl, int gb, int gpw,
-                                                const float* __restrict__ ws, float* __restrict__ xw,
-                                                const float* __restrict__ res) {
-  using G = LinfGeom<D>;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
-  const int n_groups = (n_nodes + G::NB - 1) / G::NB;
-  const int g_base = gb * LINF_WAVES * gpw;
-  const int njt = sl.n_out / 32, wld = sl.n_out;
-  const int xoff = sl.src[0].x_off;
-  int nq = 0;
-  for (int k = 0; k < gpw; ++k) nq += (g_base + k * LINF_WAVES + wave < n_groups);
-  if (nq == 0) return;
-  const bool row_ok = i < G::NB * D;
-  const int abase = (i / D) * G::SX + (i % D) + hf * D;
-  auto load = [&](int q, float4* r) {
-    const int n0 = (g_base + q * LINF_WAVES + wave) * G::NB;
-#pragma unroll
-    for (int qq = 0; qq < G::NQ; ++qq) {
-      const int f = lane + 64 * qq;
-      const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-      const bool ok = f < G::NB * G::RUN4 && n0 + a < n_nodes;
-      r[qq] = ok ? *reinterpret_cast<const float4*>(x + (size_t)(n0 + a) * x_row + xoff + 4 * w4)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  float4 r[G::NQ];
-  load(0, r);
-  for (int q = 0; q < nq; ++q) {
-    const int n0 = (g_base + q * LINF_WAVES + wave) * G::NB;
-#pragma unroll
-    for (int qq = 0; qq < G::NQ; ++qq) {
-      const int f = lane + 64 * qq;
-      if (f < G::NB * G::RUN4) {
-        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-        *reinterpret_cast<float4*>(xw + a * G::SX + 4 * w4) = r[qq];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    float av[16];
-#pragma unroll
-    for (int st = 0; st < 16; ++st) av[st] = row_ok ? xw[abase + 2 * st * D] : 0.0f;
-    __builtin_amdgcn_wave_barrier();
-    if (q + 1 < nq) load(q + 1, r);   // in flight during the column tiles
-    for (int jt = 0; jt < njt; ++jt) {
-      const float bj = (sl.bias_off >= 0 && D == 1) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
-      eelg_f32x16 acc;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) acc[t] = bj;
-      const float* __restrict__ wk = ws + hf * wld + jt * 32 + i;
-#pragma unroll
-      for (int st = 0; st < 16; ++st)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], wk[2 * st * wld], acc, 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const int row = (t & 3) + 8 * (t >> 2) + 4 * hf;
-        const int n = row / D, m = row - (row / D) * D;
-        if (row < G::NB * D) xw[n * G::SX + i * D + m] = acc[t];
-      }
-      __builtin_amdgcn_wave_barrier();
-      const size_t tile_off = sl.y_off + (size_t)jt * 32 * D;
-#pragma unroll
-      for (int qq = 0; qq < G::NQ; ++qq) {
-        const int f = lane + 64 * qq;
-        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-        if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
-          const size_t o = (size_t)(n0 + a) * y_row + tile_off + 4 * w4;
-          float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
-          if (res) {
-            const float4 r4 = *reinterpret_cast<const float4*>(res + o);
-            v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
-          }
-          *reinterpret_cast<float4*>(y + o) = v;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-}
-
-__global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_jl_kernel(
-    const float* __restrict__ x, int x_row, const float* __restrict__ w,
-    const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
-    eelg_lin_desc desc, const float* __restrict__ res, int gpw) {
-  __shared__ float ws[LINF_KMAX * 32];
-  __shared__ float4 xw4[LINF_WAVES * LINF_XW / 4];
-  const eelg_lin_slot& sl = desc.slot[desc.n_slots - 1 - blockIdx.y];
-  // group blocks in XCD order: consecutive group blocks (adjacent node rows) on one XCD
-  const int id = blockIdx.x, gb = (id >> 3) + (id & 7) * (gridDim.x >> 3);
-  const int d = sl.d;
-  const int n_groups = (n_nodes + 32 / d - 1) / (32 / d);
-  if (gb * LINF_WAVES * gpw >= n_groups) return;   // uniform per workgroup
-  // all column tiles: ws[k][j] = alpha * W[k][j], row stride n_out
-  const eelg_lin_src& src = sl.src[0];
-  const int no = sl.n_out;
-  for (int e = threadIdx.x; e < 32 * no; e += 64 * LINF_WAVES) {
-    const int k = e / no, jj = e - k * no;
-    ws[e] = w[src.w_off + (size_t)k * src.ldk + (size_t)jj * src.ldj] * src.alpha;
-  }
-  __syncthreads();
-  float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
-  switch (d) {
-    case 1: lin_fwd_fast_jl<1>(x, x_row, bias, n_nodes, y, y_row, sl, gb, gpw, ws, xw, res); break;
-    case 3: lin_fwd_fast_jl<3>(x, x_row, bias, n_nodes, y, y_row, sl, gb, gpw, ws, xw, res); break;
-    case 5: lin_fwd_fast_jl<5>(x, x_row, bias, n_nodes, y, y_row, sl, gb, gpw, ws, xw, res); break;
-    case 7: lin_fwd_fast_jl<7>(x, x_row, bias, n_nodes, y, y_row, sl, gb, gpw, ws, xw, res); break;
-    default: lin_fwd_fast_jl<9>(x, x_row, bias, n_nodes, y, y_row, sl, gb, gpw, ws, xw, res); break;
-  }
-}
-
-#ifndef LINF_JL_GPW
-#define LINF_JL_GPW 0          // node groups per wave in the column-tile loop variant
-#endif
-// EELG_LIN_JL_GPW overrides the groups per wave (0: column tiles as separate workgroups)
-static int lin_jl_gpw() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("EELG_LIN_JL_GPW");
-    v = e ? atoi(e) : LINF_JL_GPW;
-    if (v < 0) v = 0;
-  }
-  return v;
-}
-
-// the column-tile loop applies when every slot's sources are one 32-wide K chunk and there
-// are several column tiles whose weights fit LDS
-static bool lin_fwd_jl_ok(const eelg_lin_desc* desc) {
-  if (desc->max_jt < 2) return false;
-  for (int s = 0; s < desc->n_slots; ++s) {
-    const eelg_lin_slot& sl = desc->slot[s];
-    if (sl.n_src != 1 || sl.src[0].k != 32 || sl.n_out > LINF_KMAX) return false;
-  }
-  return true;
-}
-
 __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
     const float* __restrict__ x, int x_row, const float* __restrict__ w,
     const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
@@ -827,101 +684,10 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   lin_fwd_fast_d(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
 }
 
-// Balanced form for one column tile per slot (the 7360 -> 800 and 800 -> 800 linears): the
-// grid is sized to the resident workgroups and split over the slots in proportion to their
-// cost (node groups x K chunks; plan.wg_end = the running workgroup counts, slots heavy
-// first); a slot's workgroups take equal contiguous ranges of its node groups.  No partially
-// filled last round of workgroups, and the weight tile is staged once per workgroup instead
-// of once per 32 node groups.
-struct eelg_lin_bal_plan { int wg_end[EELG_LIN_MAXSLOT]; };
-
-__global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_bal_kernel(
-    const float* __restrict__ x, int x_row, const float* __restrict__ w,
-    const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
-    eelg_lin_desc desc, const float* __restrict__ res, int ws4, eelg_lin_bal_plan plan) {
-  extern __shared__ float4 linf_smem[];
-  float* ws = reinterpret_cast<float*>(linf_smem);
-  float* xw = reinterpret_cast<float*>(linf_smem + ws4) + (threadIdx.x >> 6) * LINF_XW;
-  int o = 0;
-  while (o + 1 < desc.n_slots && (int)blockIdx.x >= plan.wg_end[o]) ++o;
-  const int wg0 = o ? plan.wg_end[o - 1] : 0, nwg = plan.wg_end[o] - wg0, j = blockIdx.x - wg0;
-  const eelg_lin_slot& sl = desc.slot[desc.n_slots - 1 - o];
-  const int ng = (n_nodes + 32 / sl.d - 1) / (32 / sl.d);
-  const int g0 = (int)((long long)ng * j / nwg), g1 = (int)((long long)ng * (j + 1) / nwg);
-  if (g0 >= g1) return;   // uniform per workgroup
-  int kb = 0;
-  for (int t = 0; t < sl.n_src; ++t) {
-    const eelg_lin_src& src = sl.src[t];
-    for (int e = threadIdx.x; e < src.k * 32; e += 64 * LINF_WAVES) {
-      const int k = e >> 5, jj = e & 31;
-      ws[(kb + k) * 32 + jj] = w[src.w_off + (size_t)k * src.ldk + (size_t)jj * src.ldj] * src.alpha;
-    }
-    kb += src.k;
-  }
-  __syncthreads();
-  lin_fwd_fast_d(sl.d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, 0, ws, xw, res);
-}
-
-// workgroups per slot (slots heavy first) for lin_fwd_bal_kernel: proportional to cost
-static void lin_bal_plan(const eelg_lin_desc* desc, int n_nodes, int total_wg, eelg_lin_bal_plan* p) {
-  long long cost[EELG_LIN_MAXSLOT], total = 0;
-  for (int o = 0; o < desc->n_slots; ++o) {
-    const eelg_lin_slot& sl = desc->slot[desc->n_slots - 1 - o];
-    int nch = 0;
-    for (int t = 0; t < sl.n_src; ++t) nch += sl.src[t].k / 32;
-    cost[o] = (long long)((n_nodes + 32 / sl.d - 1) / (32 / sl.d)) * nch;
-    total += cost[o];
-  }
-  long long acc = 0;
-  int prev = 0;
-  for (int o = 0; o < desc->n_slots; ++o) {
-    acc += cost[o];
-    int e = (int)((acc * total_wg + total / 2) / (total > 0 ? total : 1));
-    if (e < prev + 1) e = prev + 1;   // every slot gets a workgroup
-    p->wg_end[o] = prev = e;
-  }
-}
-
-#ifndef LINF_LDS_1JT
-#define LINF_LDS_1JT (64 * 1024)   // LDS floor with one column tile per slot (two workgroups per CU)
-#endif
-// EELG_LINF_LDS_FLOOR (bytes): a floor on the dynamic LDS of every launch (A/B of occupancy)
-static size_t lin_lds_floor() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("EELG_LINF_LDS_FLOOR");
-    v = e ? atol(e) : 0;
-    if (v < 0) v = 0;
-  }
-  return (size_t)v;
-}
-static size_t lin_lds_1jt() {   // EELG_LINF_LDS_1JT overrides LINF_LDS_1JT
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("EELG_LINF_LDS_1JT");
-    v = e ? atol(e) : LINF_LDS_1JT;
-    if (v < 0) v = 0;
-  }
-  return (size_t)v;
-}
-#ifndef LINF_BAL_MAXWG
-#define LINF_BAL_MAXWG 3           // resident 8-wave workgroups per CU (VGPR-limited at <= 85 VGPRs)
-#endif
-#ifndef LINF_BAL_ROUNDS
-#define LINF_BAL_ROUNDS 0   // off: 1 and 4 measured slower in the training step (r02 ab_bal2)
-#endif
-// EELG_LIN_BAL: workgroups of the balanced grid in units of the resident count (0: the
-// one-workgroup-per-32-groups grid).  Side-stream kernels share the CUs in the training step,
-// so a grid of exactly the resident count leaves a tail behind the slowest CU.
-static int lin_bal_rounds() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("EELG_LIN_BAL");
-    v = e ? atoi(e) : LINF_BAL_ROUNDS;
-    if (v < 0) v = 0;
-  }
-  return v;
-}
+// one column tile per slot (the 800 -> 800 linears): an LDS floor of 64 KB (two workgroups per
+// CU) measured faster than three.  Tried and removed: a column-tile loop
+// for the K = 32 grad-x, and a cost-balanced resident grid for the single-tile linears.
+#define LINF_LDS_1JT (64 * 1024)
 // weight region (float4) and total dynamic LDS bytes of lin_fwd_fast_kernel for a descriptor
 static void lin_fwd_fast_lds(const eelg_lin_desc* desc, int* ws4, size_t* bytes) {
   int kmax = 0;

@@ -181,13 +181,12 @@ def _tp_info(idx: int):
 
 
 def _sc_info(idx: int):
-    info = (ctypes.c_int * 9)()
+    info = (ctypes.c_int * 7)()
     sig = ctypes.c_uint64()
     rc = load().eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P))
     if rc != 0:
         return None
-    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk", "coef_mulmajor",
-            "coef_pairs")
+    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk")
     return dict(zip(keys, list(info))), sig.value
 
 

@@ -407,11 +407,8 @@ class _SymCon(torch.autograd.Function):
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
         out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
-        # two-channels-per-lane forward: coefficients channel-pair interleaved [mul/2, nt, 2]
-        cf = (coef.view(mul // 2, 2, -1).transpose(1, 2).contiguous()
-              if info.get("coef_pairs", 0) else coef)
         tok = TIMER.start("sc_fwd")
-        _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(cf), n, mul, _lib.ptr(out),
+        _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),
                                    _lib.stream(out)), "sc_fwd")
         TIMER.stop(tok)
         ctx.save_for_backward(x, coef)
@@ -426,17 +423,14 @@ class _SymCon(torch.autograd.Function):
         lib = _lib.load()
         gx = gcoef = None
         want_x, want_c = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        # the coefficient gradient reads the mul-major x / grad_out rows itself (coef_mulmajor),
-        # or channel-major copies that grad-x writes from the tiles it stages anyway
-        mulmajor = bool(ctx.info.get("coef_mulmajor", 0))
-        if want_c and mulmajor:
-            xt, gt = x, g
-        elif want_c:
+        # the coefficient gradient reads channel-major copies of x / grad_out, which grad-x
+        # writes from the tiles it stages anyway
+        if want_c:
             xt = torch.empty(ctx.mul * ctx.info["D"], n, device=x.device, dtype=torch.float32)
             gt = torch.empty(ctx.mul * ctx.info["Dout"], n, device=x.device, dtype=torch.float32)
         # with a side stream, the channel-major transposes move there with the coef-grad
         # (off the main chain); in line, grad-x writes them from the tiles it stages anyway
-        cm_side = want_c and not mulmajor and ctx.side is not None and SC_CMAJOR_ON_SIDE
+        cm_side = want_c and ctx.side is not None and SC_CMAJOR_ON_SIDE
         if cm_side:
             # launched before grad-x: the transposes need only x and grad_out, and run beside it
             side = ctx.side
@@ -451,7 +445,7 @@ class _SymCon(torch.autograd.Function):
         if want_x:
             gx = torch.empty_like(x)
             tok = TIMER.start("sc_bwd_x")
-            fuse = want_c and not cm_side and not mulmajor
+            fuse = want_c and not cm_side
             _lib.check(lib.eelg_sc_bwd_x_cm(ctx.cfg, _lib.ptr(x), _lib.ptr(coef), _lib.ptr(g), n,
                                             ctx.mul, _lib.ptr(gx),
                                             _lib.ptr(xt) if fuse else None,
@@ -459,7 +453,7 @@ class _SymCon(torch.autograd.Function):
                        "sc_bwd_x")
             TIMER.stop(tok)
         if want_c:
-            if not (want_x or cm_side or mulmajor):
+            if not (want_x or cm_side):
                 tok = TIMER.start("sc_cmajor")
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 0, _lib.ptr(x), n, ctx.mul, _lib.ptr(xt),
                                               _lib.stream(xt)), "sc_cmajor")

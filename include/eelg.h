@@ -36,16 +36,12 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk, coef_mulmajor,
- * coef_pairs}
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk}
  * (D: coupling components per channel of the input, D_out: of the output; they differ when the
  * product maps the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node
- * chunk of eelg_sc_bwd_coef; coef_mulmajor: 1 if eelg_sc_bwd_coef takes the mul-major x /
- * grad_out rows, 0 if it takes the channel-major copies of eelg_sc_bwd_x_cm; coef_pairs: 1 if
- * eelg_sc_fwd takes the coefficients channel-pair interleaved, coef2[c/2][t][c%2], 0 if
- * [mul][nterms] like eelg_sc_bwd_x) */
+ * chunk of eelg_sc_bwd_coef) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info9, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info7, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -186,8 +182,7 @@ int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_row
 
 /* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
  * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
- * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms], or channel-pair interleaved
- * [mul/2][nterms][2] for eelg_sc_fwd when the config's coef_pairs (eelg_sc_info info[8]) is 1. */
+ * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms]. */
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
@@ -202,13 +197,12 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
 int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, float* xt,
                    void* stream);
 /* Coefficient gradient (replaces the weight gradient through the U.W contraction of
- * gnn/mace.py:242-277) from x and grad_out: the mul-major rows [N, x_row] / [N, out_row] when
- * the config's coef_mulmajor (eelg_sc_info info[7]) is 1, else their channel-major copies
- * xt[(c*D + a)*N + n] / gt (eelg_sc_bwd_x_cm).  partial[n_chunks, mul, nterms],
+ * gnn/mace.py:242-277) from the channel-major copies xt[(c*D + a)*N + n] / gt of x and
+ * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_chunks, mul, nterms],
  * n_chunks = ceil(n_nodes / chunk); chunk must be the config's coef_chunk (info[6]): one
  * workgroup keeps that many nodes of one channel resident in LDS.  The caller sums over
  * chunks (deterministic). */
-int eelg_sc_bwd_coef(int cfg, const float* x_or_xt, const float* grad_out_or_gt, int n_nodes,
+int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes,
                      int mul, int chunk, float* partial, void* stream);
 
 /* Channel-mixing linear on mul-major irreps rows (o3.Linear, gnn/blocks.py:516-521,

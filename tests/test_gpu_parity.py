@@ -370,7 +370,7 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
         blocks = [rows[:, 32 * l * l: 32 * (l + 1) ** 2].reshape(n, 32, 2 * l + 1) for l in range(lmax + 1)]
         return torch.cat(blocks, 2).permute(1, 2, 0).contiguous()          # [32, D, n]
     xt, gt = cmajor(x), cmajor(g)
-    ops_x, ops_g = (x, g) if info["coef_mulmajor"] else (xt, gt)
+    ops_x, ops_g = xt, gt
     nch = -(-n // chunk)
     part = torch.full((nch, 32, nt), float("nan"), device=DEV)
     lib = _lib.load()

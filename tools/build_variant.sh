@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a kernel variant of libeelg.so into variants/libeelg_<tag>.so with generator env overrides
 # (EELG_* knobs of csrc/gen_kernels.py) and optional EXTRA hipcc flags, through the same Makefile.
-# usage: EELG_SC_COEF_UNROLL=2 tools/build_variant.sh <tag>     (load it with EELG_LIB=...)
+# usage: EELG_TP_MAXACC=48 tools/build_variant.sh <tag>     (load it with EELG_LIB=...)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=/tmp/eelg_var_$1

@@ -2,7 +2,7 @@
 """Quick register / LDS check of one generated kernel without the full library build:
 generate with the current EELG_* env knobs, cut the preamble + the named kernel into a small
 translation unit, compile for gfx950 and print the compiler's resource-usage remarks.
-usage: EELG_TP_M_B=4 python tools/proto/kres.py tp_fwd_tpB_l4 [more kernels...]"""
+usage: EELG_TP_MAXACC=48 python tools/proto/kres.py tp_fwd_tpB_l4 [more kernels...]"""
 import os, re, subprocess, sys, tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CS = os.path.join(ROOT, "energy-equiv-lattice-gnn_amd", "csrc")
