@@ -13,7 +13,7 @@ for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$O/p$i" -o p -- \
-      python3 "$R/tools/kbench.py" --reps 3 --only "$ONLY" > "$O/p$i.log" 2>&1 || echo "pass $i failed ($grp)"
+      python3 "$R/tools/kbench.py" --reps 3 --only "$ONLY" > "$O/p$i.log" 2>&1
 done
 python3 "$R/tools/mfma_table.py" "$O" > "$O/table.md"
 cat "$O/table.md"
