@@ -637,12 +637,21 @@ int eelg_gate_bwd(const float* x, const float* grad_y, int n_nodes, const eelg_g
   return check_launch("gate_bwd");
 }
 
+// fwd / grad-x / channel-major copy: 64-node tiles x mul/4 channel quads, 1-D; the tile count
+// is padded to a multiple of 8 so the quads of tile t all run on XCD t % 8 (gen_kernels.py)
+static bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static dim3 sc_tile_grid(int n_nodes, int mul) {
+  const int tiles = (n_nodes + 63) / 64;
+  return dim3(((tiles + 7) / 8) * 8 * (mul / 4));
+}
+
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
                 void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
+  if (!a16(x) || !a16(out)) return fail(-2, "sc_fwd: x and out must be 16-byte aligned");
+  hipLaunchKernelGGL(c->fwd, sc_tile_grid(n_nodes, mul), dim3(256), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -657,7 +666,9 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_x, dim3(mul / 4, (n_nodes + c->nb - 1) / c->nb), dim3(256), 0,
+  if (!a16(x) || !a16(grad_out) || !a16(grad_x))
+    return fail(-2, "sc_bwd_x: x, grad_out and grad_x must be 16-byte aligned");
+  hipLaunchKernelGGL(c->bwd_x, sc_tile_grid(n_nodes, mul), dim3(256), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
 }
@@ -668,7 +679,8 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
   if (!c) return -1;
   if (which != 0 && which != 1) return fail(-2, "sc_cmajor: which must be 0 (input) or 1 (output)");
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(which ? c->cmajor_out : c->cmajor, dim3(mul / 4, (n_nodes + 63) / 64), dim3(256), 0,
+  if (!a16(x)) return fail(-2, "sc_cmajor: x must be 16-byte aligned");
+  hipLaunchKernelGGL(which ? c->cmajor_out : c->cmajor, sc_tile_grid(n_nodes, mul), dim3(256), 0,
                      (hipStream_t)stream, x, n_nodes, xt);
   return check_launch("sc_cmajor");
 }

@@ -49,7 +49,6 @@ struct eelg_sc_cfg {
   eelg_sc_bwdc_fn bwd_coef;
   eelg_sc_cmajor_fn cmajor;      // input (coupling) layout
   eelg_sc_cmajor_fn cmajor_out;  // output layout
-  int nb;                        // nodes per fwd / grad-x workgroup
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
 };
 

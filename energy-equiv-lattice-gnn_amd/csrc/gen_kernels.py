@@ -36,11 +36,16 @@ MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
+# tp_fwd streaming cache policy: nontemporal stores of the aggregate rows / loads of the edge
+# weights (neither is re-read by the kernel; keeps L2 for the gathered x rows)
+TP_NT_STORE = int(os.environ.get("EELG_TP_NT_STORE", "0"))
+TP_NT_W = int(os.environ.get("EELG_TP_NT_W", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
-# computed, forward / grad-x (r02: grad-x 0.56 -> 0.51 ms at 3; the forward spills SGPRs at 2+)
+# computed, forward / grad-x (r03m: grad-x 0.44 ms at 2; at 3 it spills SGPRs into VGPR lanes
+# once the staging is rewritten, 0.60 ms; the forward spills SGPRs at 2+)
 SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
-SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "3"))
+SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "2"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, the most
 # accumulators (terms) per wave
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
@@ -214,12 +219,17 @@ def vec_load(names: Sequence[str], base: str, start: str) -> List[str]:
     return out
 
 
-def vec_store(vals: Sequence[str], base: str, start: str) -> List[str]:
+def vec_store(vals: Sequence[str], base: str, start: str, nt: bool = False) -> List[str]:
+    """base[start + i] = vals[i] with dword-aligned 4/3/2-wide stores; ``nt``: nontemporal"""
     out, i = [], 0
     while i < len(vals):
         w = min(4, len(vals) - i)
         if w == 1:
-            out.append(f"{base}[{start} + {i}] = {vals[i]};")
+            out.append(f"__builtin_nontemporal_store({vals[i]}, {base} + {start} + {i});" if nt
+                       else f"{base}[{start} + {i}] = {vals[i]};")
+        elif nt:
+            out.append(f"__builtin_nontemporal_store({_VT[w]}{{" + ", ".join(vals[i: i + w])
+                       + f"}}, reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}));")
         else:
             out.append(f"*reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}) = {_VT[w]}{{"
                        + ", ".join(vals[i: i + w]) + "};")
@@ -294,11 +304,11 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("    float inv_norm, float* __restrict__ agg) {")
     L.append("  const int lane = threadIdx.x & 63;")
     L.append(f"  const int u = lane & {MUL - 1};")
-    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
     # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the x
     # rows of a lattice are gathered by one XCD (its L2) rather than by all eight (r03h: 1828
     # -> 1865 graphs/s together with the 64-accumulator groups)
     L.append(f"  const int ntl = (n_nodes + {8 * TP_NPH - 1}) / {8 * TP_NPH}, tpx = (ntl + 7) >> 3;")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
     L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
     L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
     L.append("  if (n0 >= n_nodes) return;")
@@ -327,7 +337,9 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
                                                           f"{node_off[l]} + u * {d}")]
             out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
             for p in grp:
-                out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
+                wv_ = (f"__builtin_nontemporal_load(we + {p.slot * MUL})" if TP_NT_W
+                       else f"we[{p.slot * MUL}]")
+                out.append(f"      {pref}w{p.slot} = {ld_w(wv_)};")
             out.append("    }")
             return out
         L.append("    int e = rowptr[n0];")
@@ -347,7 +359,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             for p in grp:
                 d3 = 2 * p.l3 + 1
                 out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                             f"{p.out_off} + u * {d3}"))
+                                                             f"{p.out_off} + u * {d3}", TP_NT_STORE))
             out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
             out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
             out.append("      }")
@@ -714,47 +726,78 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 
     NB = 64                                 # nodes per workgroup (fwd / grad-x), one per lane
 
+    # Staging between the mul-major rows and the quad tile.  A quad owns, per node and l-block,
+    # one run of 4*d floats (d float4, 16-B aligned), so a tile of nb nodes is nb * D float4:
+    # float4 j of a node sits at LDS column 4*j and at global float offset
+    # o_l + cq*4*d_l + 4*(j - start_l) of its l-block.  Every float4 load of a thread is issued
+    # before the first LDS store (one memory round trip per tile, not one per element), with
+    # the node index clamped in bounds instead of a branch around each load.
+    def _gofs(lay, j):
+        """select chain (v_cndmask, no branches): global float offset of quad float4 j"""
+        expr = None
+        for (s0, s1, o, d) in lay.segs:
+            st4 = s0 // 4
+            v = f"{o} + cqo_ * {4 * d} + 4 * ({j} - {st4})"
+            expr = v if expr is None else f"({j} >= {st4} ? {v} : {expr})"
+        return expr
+
     def stage_in(src, tile, lay, nb=64):
-        per = (nb * lay.QD + 255) // 256
-        out = ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
-               "#pragma unroll 2",
-               f"  for (int it = 0; it < {per}; ++it) {{",
-               "    const int idx = tid + 256 * it;",
-               f"    if (idx < {nb * lay.QD}) {{",
-               f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
-               f"      {tile}[nl * {TP} + q] = (n < n_nodes) ? {src}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] : 0.0f;",
-               "    }", "  } }"]
+        n4 = lay.QD // 4
+        tot = nb * n4
+        it_n = -(-tot // 256)
+        out = ["  { int cqo_ = cq; asm volatile(\"\" : \"+s\"(cqo_));"]
+        for it in range(it_n):
+            out.append(f"    const int i{it} = min((int)threadIdx.x + {256 * it}, {tot - 1}), "
+                       f"nl{it} = i{it} / {n4}, j{it} = i{it} - nl{it} * {n4};")
+            out.append(f"    const float4 v{it} = *reinterpret_cast<const float4*>({src} + "
+                       f"(size_t)min(n0 + nl{it}, n_nodes - 1) * {lay.row} + {_gofs(lay, f'j{it}')});")
+        for it in range(it_n):
+            # a clamped tail thread rewrites the tile's last float4 with the same value
+            out.append(f"    {{ const bool ok = n0 + nl{it} < n_nodes; "
+                       f"float* t_ = {tile} + nl{it} * {TP} + 4 * j{it}; "
+                       f"t_[0] = ok ? v{it}.x : 0.0f; t_[1] = ok ? v{it}.y : 0.0f; "
+                       f"t_[2] = ok ? v{it}.z : 0.0f; t_[3] = ok ? v{it}.w : 0.0f; }}")
+        out.append("  }")
         return out
 
     def stage_out(dst, tile, lay, nb=64):
-        per = (nb * lay.QD + 255) // 256
-        return ["  { int tid = threadIdx.x; asm volatile(\"\" : \"+v\"(tid));",
-                "#pragma unroll 2",
-                f"  for (int it = 0; it < {per}; ++it) {{",
-                "    const int idx = tid + 256 * it;",
-                f"    if (idx < {nb * lay.QD}) {{",
-                f"      const int nl = idx / {lay.QD}, q = idx - nl * {lay.QD}, n = n0 + nl;",
-                f"      if (n < n_nodes) {dst}[(size_t)n * {lay.row} + {lay.goff}(q, cq)] = {tile}[nl * {TP} + q];",
-                "    }", "  } }"]
+        n4 = lay.QD // 4
+        tot = nb * n4
+        out = ["  { int cqo_ = cq; asm volatile(\"\" : \"+s\"(cqo_));"]
+        for it in range(-(-tot // 256)):
+            out.append(f"    {{ const int i_ = (int)threadIdx.x + {256 * it}, nl_ = i_ / {n4}, j_ = i_ - nl_ * {n4};")
+            guard = f"i_ < {tot} && " if 256 * (it + 1) > tot else ""
+            out.append(f"      if ({guard}n0 + nl_ < n_nodes) {{ const float* t_ = {tile} + nl_ * {TP} + 4 * j_; "
+                       f"*reinterpret_cast<float4*>({dst} + (size_t)(n0 + nl_) * {lay.row} + {_gofs(lay, 'j_')}) = "
+                       "make_float4(t_[0], t_[1], t_[2], t_[3]); } }")
+        out.append("  }")
+        return out
 
     def cm_store(dst, tile, lay, nb, ind="  "):
         """dst[(c * D + a) * n_nodes + n] = component a of channel c of node n, from a staged
         tile of nb nodes x the quad's 4 channels (coalesced nb-float runs per (c, a))"""
         dd = lay.D
-        sgs = ", ".join(str(lay.comp[a][3]) for a in range(dd))
-        dls = ", ".join(str(2 * lay.comp[a][0] + 1) for a in range(dd))
-        ms = ", ".join(str(lay.comp[a][1]) for a in range(dd))
         sh = nb.bit_length() - 1
-        per = (Q * dd * nb + 255) // 256
-        out = [f"{{ const int kseg[{dd}] = {{{sgs}}}, kd[{dd}] = {{{dls}}}, km[{dd}] = {{{ms}}};",
-               f"  for (int it = 0; it < {per}; ++it) {{",
-               "    const int idx = threadIdx.x + 256 * it;",
-               f"    if (idx < {Q * dd * nb}) {{",
-               f"      const int row = idx >> {sh}, nl = idx & {nb - 1}, n = n0 + nl;",
-               f"      const int cl = row / {dd}, a = row - cl * {dd};",
-               f"      if (n < n_nodes) {dst}[(size_t)((cq * {Q} + cl) * {dd} + a) * n_nodes + n] = "
-               f"{tile}[nl * {TP} + kseg[a] + cl * kd[a] + km[a]];",
-               "    }", "  } }"]
+        tot = Q * dd * nb
+
+        def col():
+            # LDS column of row r = cl * D + a: seg_start(a) + cl * d(a) + m(a), a select chain
+            expr = None
+            for (s0, s1, o, d) in lay.segs:
+                a0 = s0 // 4                       # first component of this l-block
+                v = f"{s0} + cl_ * {d} + (a_ - {a0})"
+                expr = v if expr is None else f"(a_ >= {a0} ? {v} : {expr})"
+            return expr
+        # a rolled loop: its per-row address arithmetic stays inside (unrolled, the uniform row
+        # values were hoisted to the kernel top and spilled SGPRs in grad-x)
+        out = ["{ int tid_ = threadIdx.x; asm volatile(\"\" : \"+v\"(tid_));",
+               "#pragma unroll 1",
+               f"  for (int i_ = tid_; i_ < {tot}; i_ += 256) {{",
+               f"    const int row_ = i_ >> {sh}, nl_ = i_ & {nb - 1};",
+               f"    const int cl_ = row_ / {dd}, a_ = row_ - cl_ * {dd};",
+               f"    if (n0 + nl_ < n_nodes) {dst}[(size_t)((cq * {Q} + cl_) * {dd} + a_) * n_nodes + n0 + nl_] = "
+               f"{tile}[nl_ * {TP} + {col()}];",
+               "  }", "}"]
         return [ind + ln for ln in out]
 
     # group terms by (a, b) pair
@@ -770,7 +813,16 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             else:
                 g["d3"].setdefault(c, []).append((t, q))
 
-    head = ["  const int cq = blockIdx.x;", f"  const int n0 = blockIdx.y * {NB};",
+    # block id -> (node tile, channel quad): the MUL / 4 quad workgroups of one node tile run on
+    # one XCD (blockIdx % 8), so the lines of the tile's rows that several quads share (a quad
+    # owns a 16*d-byte run of each 128*d-byte l-block) are fetched from HBM once, into that
+    # XCD's L2, and its partial-line stores merge there
+    NQ = MUL // Q
+    tile_map = ["  const int xcd = blockIdx.x & 7, rest_ = blockIdx.x >> 3;",
+                f"  const int cq = rest_ % {NQ};",
+                f"  const int n0 = ((rest_ / {NQ}) * 8 + xcd) * 64;",
+                "  if (n0 >= n_nodes) return;   // uniform per workgroup (tile count padded to 8)"]
+    head = tile_map + [
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
             f"  const int cl = __builtin_amdgcn_readfirstlane(wv & {Q - 1});",
@@ -897,8 +949,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"__global__ __launch_bounds__(256) void {kname}(")
         L.append("    const float* __restrict__ x, int n_nodes, float* __restrict__ xt) {")
         L.append(f"  __shared__ float tile[64 * {TP}];")
-        L.append("  const int cq = blockIdx.x;")
-        L.append("  const int n0 = blockIdx.y * 64;")
+        L.extend(tile_map)
         L.extend(stage_in("x", "tile", lay))
         L.append("  __syncthreads();")
         L.extend(cm_store("xt", "tile", lay, 64))
@@ -1010,7 +1061,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nb=NB, nbc=NBC,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nbc=NBC,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -1050,7 +1101,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nb"]}, {i["nbc"]}}},')
+                     f'{i["cmajor_out"]}, {i["nbc"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

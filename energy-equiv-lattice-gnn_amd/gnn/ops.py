@@ -93,6 +93,13 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+def _a16(t: torch.Tensor) -> torch.Tensor:
+    """contiguous fp32 with a 16-byte aligned data pointer (float4 row access), copying a
+    misaligned view"""
+    t = _f32(t)
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def _i32(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.int32).contiguous()
 
@@ -401,7 +408,7 @@ def in_degree_scale(csr: EdgeCSR) -> torch.Tensor:
 class _SymCon(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int, side=None):
-        x, coef = _f32(x), _f32(coef)
+        x, coef = _a16(x), _f32(coef)
         n = x.shape[0]
         if x.shape[1] != info["x_row"] or coef.shape != (mul, info["nterms"]):
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
@@ -418,7 +425,7 @@ class _SymCon(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, coef = ctx.saved_tensors
-        g = _f32(g)
+        g = _a16(g)
         n = x.shape[0]
         lib = _lib.load()
         gx = gcoef = None

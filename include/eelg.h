@@ -182,7 +182,8 @@ int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_row
 
 /* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
  * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
- * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms]. */
+ * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms].  The row tensors (x, out, grad_out,
+ * grad_x) must be 16-byte aligned (float4 row access); a misaligned pointer returns -2. */
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,

@@ -315,6 +315,39 @@ def test_symcon_grad_x_writes_channel_major_copies(n):
     torch.cuda.synchronize()
     assert torch.equal(gx0, gx1)
     assert torch.equal(xt0, xt1) and torch.equal(gt0, gt1)
+    # the transposes themselves: xt[(c * 25 + a), n] = component a of channel c of node n
+    blocks = [x[:, 32 * l * l: 32 * (l + 1) ** 2].reshape(n, 32, 2 * l + 1) for l in range(5)]
+    assert torch.equal(xt0, torch.cat(blocks, 2).permute(1, 2, 0).reshape(800, n))
+
+
+def test_symcon_misaligned_rows():
+    """The contraction kernels read and write rows as float4: a row tensor that is a view at a
+    4-byte offset is copied by the host op (same result, bitwise), and the C-ABI rejects it."""
+    from gnn import _lib, ops
+    from gnn.mace import SymmetricContraction
+    torch.manual_seed(3)
+    hid = "32x0e+32x1o+32x2e+32x3o+32x4e"
+    sc = SymmetricContraction(hid, hid, 3).to(DEV)
+    idx, info = sc._config()
+    coef = sc.coefficients().detach()
+    n = 333
+    buf = torch.randn(n * 800 + 1, device=DEV)
+    xm = buf[1:].view(n, 800)
+    assert xm.data_ptr() % 16 != 0
+    xa = xm.clone()
+    xm.requires_grad_(True)
+    xa.requires_grad_(True)
+    ym = ops.symmetric_contraction(xm, coef, idx, info, 32)
+    ya = ops.symmetric_contraction(xa, coef, idx, info, 32)
+    g = torch.randn_like(ya)
+    ym.backward(g)
+    ya.backward(g)
+    assert torch.equal(ym, ya) and torch.equal(xm.grad, xa.grad)
+    lib = _lib.load()
+    out = torch.empty(n, 800, device=DEV)
+    with pytest.raises(_lib.EELGError):
+        _lib.check(lib.eelg_sc_fwd(idx, _lib.ptr(xm), _lib.ptr(coef), n, 32, _lib.ptr(out),
+                                   _lib.stream(out)), "sc_fwd")
 
 
 def test_stream_overlap_matches_in_line_bitwise():

@@ -48,3 +48,7 @@ with tempfile.TemporaryDirectory() as d:
             print(ln.split("remark: ")[-1])
     if r.returncode:
         print(r.stderr[-3000:])
+    if os.environ.get("KRES_ASM"):   # also write the kernel's assembly there
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                        "-fno-slp-vectorize", "--cuda-device-only", "-S", "-o", os.environ["KRES_ASM"], tu],
+                       check=True)
