@@ -519,6 +519,27 @@ struct LinfGeom {
   static constexpr int NQ = (NB * RUN4 + 63) / 64;          // float4 loads per lane per chunk
 };
 
+// ws[k][j] = alpha * W[k][jt*32 + j] for one source: BATCH loads per thread issued before their
+// LDS stores (clamped indices, guarded stores)
+template <int BATCH>
+__device__ __forceinline__ void lin_stage_w(const float* __restrict__ w, const eelg_lin_src& src,
+                                            int jt, float* __restrict__ ws) {
+  const int tot = src.k * 32;
+  for (int e0 = threadIdx.x; e0 < tot; e0 += BATCH * 64 * LINF_WAVES) {
+    float v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int e = min(e0 + u * 64 * LINF_WAVES, tot - 1), k = e >> 5, jj = e & 31;
+      v[u] = w[src.w_off + (size_t)k * src.ldk + (size_t)(jt * 32 + jj) * src.ldj];
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int e = e0 + u * 64 * LINF_WAVES;
+      if (e < tot) ws[e] = v[u] * src.alpha;
+    }
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
                                              const float* __restrict__ bias, int n_nodes,
@@ -600,6 +621,18 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       }
       __builtin_amdgcn_wave_barrier();
       float* __restrict__ yb = y + sl.y_off + (size_t)jt * 32 * D;
+      // residual (same layout as y) added in the epilogue: all of a lane's residual loads are
+      // issued before its first store (clamped rows, no branch around a load)
+      float4 rr[G::NQ];
+      if (res) {
+        const float* __restrict__ rb = res + sl.y_off + (size_t)jt * 32 * D;
+#pragma unroll
+        for (int qq = 0; qq < G::NQ; ++qq) {
+          const int f = min(lane + 64 * qq, G::NB * G::RUN4 - 1);
+          const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+          rr[qq] = *reinterpret_cast<const float4*>(rb + (size_t)min(n0 + a, n_nodes - 1) * y_row + 4 * w4);
+        }
+      }
 #pragma unroll
       for (int qq = 0; qq < G::NQ; ++qq) {
         const int f = lane + 64 * qq;
@@ -607,10 +640,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
         if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
           const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
           float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
-          if (res) {   // residual (same layout as y) added in the epilogue
-            const float4 r4 = *reinterpret_cast<const float4*>(res + sl.y_off + (size_t)jt * 32 * D + o);
-            v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
-          }
+          if (res) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
           *reinterpret_cast<float4*>(yb + o) = v;
         }
       }
@@ -669,13 +699,13 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   const int n_groups = (n_nodes + nb - 1) / nb;
   if (gb * LINF_WAVES * LINF_GPW >= n_groups) return;   // uniform per workgroup
   // weight tile: ws[kb + k][j] = alpha_s * W_s[k][jt*32 + j] over the slot's sources
+  // (a source's loads in flight together: batches of 8 per thread, or of 2 when K = 32;
+  // clamped indices, guarded stores)
   int kb = 0;
   for (int s = 0; s < sl.n_src; ++s) {
     const eelg_lin_src& src = sl.src[s];
-    for (int e = threadIdx.x; e < src.k * 32; e += 64 * LINF_WAVES) {
-      const int k = e >> 5, jj = e & 31;
-      ws[(kb + k) * 32 + jj] = w[src.w_off + (size_t)k * src.ldk + (size_t)(jt * 32 + jj) * src.ldj] * src.alpha;
-    }
+    if (src.k == 32) lin_stage_w<2>(w, src, jt, ws + kb * 32);
+    else lin_stage_w<8>(w, src, jt, ws + kb * 32);
     kb += src.k;
   }
   __syncthreads();

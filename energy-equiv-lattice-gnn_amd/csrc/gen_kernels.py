@@ -36,10 +36,6 @@ MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
-# tp_fwd streaming cache policy: nontemporal stores of the aggregate rows / loads of the edge
-# weights (neither is re-read by the kernel; keeps L2 for the gathered x rows)
-TP_NT_STORE = int(os.environ.get("EELG_TP_NT_STORE", "0"))
-TP_NT_W = int(os.environ.get("EELG_TP_NT_W", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, forward / grad-x (r03m: grad-x 0.44 ms at 2; at 3 it spills SGPRs into VGPR lanes
@@ -219,17 +215,13 @@ def vec_load(names: Sequence[str], base: str, start: str) -> List[str]:
     return out
 
 
-def vec_store(vals: Sequence[str], base: str, start: str, nt: bool = False) -> List[str]:
-    """base[start + i] = vals[i] with dword-aligned 4/3/2-wide stores; ``nt``: nontemporal"""
+def vec_store(vals: Sequence[str], base: str, start: str) -> List[str]:
+    """base[start + i] = vals[i] with dword-aligned 4/3/2-wide stores"""
     out, i = [], 0
     while i < len(vals):
         w = min(4, len(vals) - i)
         if w == 1:
-            out.append(f"__builtin_nontemporal_store({vals[i]}, {base} + {start} + {i});" if nt
-                       else f"{base}[{start} + {i}] = {vals[i]};")
-        elif nt:
-            out.append(f"__builtin_nontemporal_store({_VT[w]}{{" + ", ".join(vals[i: i + w])
-                       + f"}}, reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}));")
+            out.append(f"{base}[{start} + {i}] = {vals[i]};")
         else:
             out.append(f"*reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}) = {_VT[w]}{{"
                        + ", ".join(vals[i: i + w]) + "};")
@@ -337,9 +329,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
                                                           f"{node_off[l]} + u * {d}")]
             out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
             for p in grp:
-                wv_ = (f"__builtin_nontemporal_load(we + {p.slot * MUL})" if TP_NT_W
-                       else f"we[{p.slot * MUL}]")
-                out.append(f"      {pref}w{p.slot} = {ld_w(wv_)};")
+                out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             out.append("    }")
             return out
         L.append("    int e = rowptr[n0];")
@@ -359,7 +349,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             for p in grp:
                 d3 = 2 * p.l3 + 1
                 out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                             f"{p.out_off} + u * {d3}", TP_NT_STORE))
+                                                             f"{p.out_off} + u * {d3}"))
             out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
             out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
             out.append("      }")
@@ -988,6 +978,24 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  const int nb = ch * {NCB};")
     L.append(f"  const int cnt = min({NCB}, n_nodes - nb);")
     L.append("  const bool vec = (n_nodes & 3) == 0;")
+    # whole aligned chunks (all but a ragged last one): every float4 load of a thread issued
+    # before its first LDS store, one memory round trip; a clamped tail thread rewrites the
+    # last float4 with the same value
+    tot4 = (D + Dout) * NC4
+    it_n = -(-tot4 // (64 * WV))
+
+    def src_row(i):
+        return (f"(a{i} < {D} ? xt + ((size_t)c * {D} + a{i}) * n_nodes : "
+                f"gt + ((size_t)c * {Dout} + (a{i} - {D})) * n_nodes)")
+    L.append(f"  if (vec && cnt == {NCB}) {{")
+    for it in range(it_n):
+        L.append(f"    const int i{it} = min((int)threadIdx.x + {64 * WV * it}, {tot4 - 1}), "
+                 f"a{it} = i{it} / {NC4}, j{it} = 4 * (i{it} - a{it} * {NC4});")
+        L.append(f"    const float4 v{it} = *reinterpret_cast<const float4*>({src_row(it)} + nb + j{it});")
+    for it in range(it_n):
+        L.append(f"    *reinterpret_cast<float4*>(a{it} < {D} ? sx + a{it} * {NCB} + j{it} : "
+                 f"sg + (a{it} - {D}) * {NCB} + j{it}) = v{it};")
+    L.append("  } else {")
     L.append(f"  for (int i = threadIdx.x; i < {(D + Dout) * NC4}; i += {64 * WV}) {{")
     L.append(f"    const int a = i / {NC4}, j = 4 * (i - a * {NC4});")
     L.append(f"    const float* __restrict__ src = a < {D} ? xt + ((size_t)c * {D} + a) * n_nodes"
@@ -1003,6 +1011,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("      if (j + 3 < cnt) v.w = src[nb + j + 3];")
     L.append("    }")
     L.append("    *reinterpret_cast<float4*>(sdst) = v;")
+    L.append("  }")
     L.append("  }")
     L.append("  __syncthreads();")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
