@@ -637,11 +637,11 @@ int eelg_gate_bwd(const float* x, const float* grad_y, int n_nodes, const eelg_g
   return check_launch("gate_bwd");
 }
 
-// fwd / grad-x / channel-major copy: 64-node tiles x mul/4 channel quads, 1-D; the tile count
+// fwd / grad-x / channel-major copy: nb-node tiles x mul/4 channel quads, 1-D; the tile count
 // is padded to a multiple of 8 so the quads of tile t all run on XCD t % 8 (gen_kernels.py)
 static bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-static dim3 sc_tile_grid(int n_nodes, int mul) {
-  const int tiles = (n_nodes + 63) / 64;
+static dim3 sc_tile_grid(int n_nodes, int mul, int nb = 64) {
+  const int tiles = (n_nodes + nb - 1) / nb;
   return dim3(((tiles + 7) / 8) * 8 * (mul / 4));
 }
 
@@ -651,7 +651,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
   if (!a16(x) || !a16(out)) return fail(-2, "sc_fwd: x and out must be 16-byte aligned");
-  hipLaunchKernelGGL(c->fwd, sc_tile_grid(n_nodes, mul), dim3(256), 0,
+  hipLaunchKernelGGL(c->fwd, sc_tile_grid(n_nodes, mul, c->nb), dim3(c->nth), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
 }
@@ -668,7 +668,7 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
   if (n_nodes <= 0) return 0;
   if (!a16(x) || !a16(grad_out) || !a16(grad_x))
     return fail(-2, "sc_bwd_x: x, grad_out and grad_x must be 16-byte aligned");
-  hipLaunchKernelGGL(c->bwd_x, sc_tile_grid(n_nodes, mul), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_x, sc_tile_grid(n_nodes, mul, c->nb), dim3(c->nth), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
 }
@@ -731,13 +731,19 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
     if (desc->max_jt == 1 && lds < LINF_LDS_1JT) lds = LINF_LDS_1JT;
     static bool lds_attr = false;   // > 64 KB of dynamic LDS must be allowed explicitly
     if (!lds_attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         return fail(-3, "linear_fwd: cannot raise the dynamic LDS limit");
       lds_attr = true;
     }
-    hipLaunchKernelGGL(lin_fwd_fast_kernel, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream, x,
-                       x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
+    if (res)
+      hipLaunchKernelGGL(lin_fwd_fast_kernel<true>, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
+                         x, x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
+    else
+      hipLaunchKernelGGL(lin_fwd_fast_kernel<false>, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
+                         x, x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
     return check_launch("linear_fwd");
   }
   dim3 grid((desc->max_rows + 127) / 128, desc->n_slots, 1);  // column tiles loop in-kernel

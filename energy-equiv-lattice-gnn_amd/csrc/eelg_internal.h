@@ -50,6 +50,8 @@ struct eelg_sc_cfg {
   eelg_sc_cmajor_fn cmajor;      // input (coupling) layout
   eelg_sc_cmajor_fn cmajor_out;  // output layout
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
+  int nb;                        // nodes per fwd / grad-x workgroup
+  int nth;                       // threads per fwd / grad-x workgroup
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -540,7 +540,7 @@ __device__ __forceinline__ void lin_stage_w(const float* __restrict__ w, const e
   }
 }
 
-template <int D>
+template <int D, bool RES>
 __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
                                              const float* __restrict__ bias, int n_nodes,
                                              float* __restrict__ y, int y_row,
@@ -624,7 +624,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       // residual (same layout as y) added in the epilogue: all of a lane's residual loads are
       // issued before its first store (clamped rows, no branch around a load)
       float4 rr[G::NQ];
-      if (res) {
+      if (RES) {
         const float* __restrict__ rb = res + sl.y_off + (size_t)jt * 32 * D;
 #pragma unroll
         for (int qq = 0; qq < G::NQ; ++qq) {
@@ -640,7 +640,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
         if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
           const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
           float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
-          if (res) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
+          if (RES) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
           *reinterpret_cast<float4*>(yb + o) = v;
         }
       }
@@ -661,6 +661,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   }
 }
 
+template <bool RES>
 __device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ x, int x_row,
                                                const float* __restrict__ bias, int n_nodes,
                                                float* __restrict__ y, int y_row,
@@ -668,14 +669,17 @@ __device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ 
                                                const float* __restrict__ ws, float* __restrict__ xw,
                                                const float* __restrict__ res) {
   switch (d) {
-    case 1: lin_fwd_fast<1>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 3: lin_fwd_fast<3>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 5: lin_fwd_fast<5>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 7: lin_fwd_fast<7>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    default: lin_fwd_fast<9>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 1: lin_fwd_fast<1, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 3: lin_fwd_fast<3, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 5: lin_fwd_fast<5, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 7: lin_fwd_fast<7, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    default: lin_fwd_fast<9, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
   }
 }
 
+// RES: the residual epilogue (y = x W + res), a separate instantiation so the plain linears
+// carry no residual registers
+template <bool RES>
 __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
     const float* __restrict__ x, int x_row, const float* __restrict__ w,
     const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
@@ -711,7 +715,7 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   __syncthreads();
   float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
   const int g0 = gb * LINF_WAVES * LINF_GPW, g1 = min(n_groups, g0 + LINF_WAVES * LINF_GPW);
-  lin_fwd_fast_d(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
+  lin_fwd_fast_d<RES>(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
 }
 
 // one column tile per slot (the 800 -> 800 linears): an LDS floor of 64 KB (two workgroups per

@@ -41,7 +41,11 @@ TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave
 # computed, forward / grad-x (r03m: grad-x 0.44 ms at 2; at 3 it spills SGPRs into VGPR lanes
 # once the staging is rewritten, 0.60 ms; the forward spills SGPRs at 2+)
 SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
+SC_BLOCK = int(os.environ.get("EELG_SC_BLOCK", "32"))     # terms per coefficient block
 SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "2"))
+# fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
+# consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
+SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, the most
 # accumulators (terms) per wave
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
@@ -623,9 +627,11 @@ def pin(vs: List[str], memory: bool = False, sgprs: Sequence[str] = ()) -> str:
 
 
 def sc_blocks(plan, maxb: int = 32) -> List[Dict]:
-    """Split the polynomial terms into blocks of <= maxb terms (one (a, b) group may span
-    several blocks; a c-subgroup is never split).  Each block's coefficients are
-    prefetched into SGPRs while the previous block computes."""
+    """Pack the polynomial terms into blocks of <= maxb terms, in term order.  A block holds
+    the deg-1 terms or a run of (a, b) pair segments: several whole pairs, or part of one (a
+    pair is split only at c-subgroup boundaries, and a c-subgroup longer than maxb stays whole).
+    Each block's coefficients are prefetched into SGPRs while earlier blocks compute, so blocks
+    of similar size keep that prefetch distance even where the pairs are small."""
     deg1, pairs = [], {}
     for t, (nu, (a, b, c), q) in enumerate(plan.terms):
         if nu == 1:
@@ -639,18 +645,31 @@ def sc_blocks(plan, maxb: int = 32) -> List[Dict]:
     blocks = []
     if deg1:
         blocks.append({"kind": "deg1", "terms": [t for t, _, _ in deg1], "deg1": deg1})
+    cur = None
+
+    def new_block():
+        blk = {"kind": "pairs", "segs": [], "terms": []}
+        blocks.append(blk)
+        return blk
     for (a, b), g in pairs.items():
-        cur = {"kind": "pair", "a": a, "b": b, "first": True, "last": False,
-               "d2": list(g["d2"]), "d3": [], "terms": [t for t, _ in g["d2"]]}
-        for c, lst in g["d3"].items():
-            if cur["terms"] and len(cur["terms"]) + len(lst) > maxb:
-                blocks.append(cur)
-                cur = {"kind": "pair", "a": a, "b": b, "first": False, "last": False,
-                       "d2": [], "d3": [], "terms": []}
-            cur["d3"].append((c, lst))
+        units = ([("d2", g["d2"])] if g["d2"] else []) + [(c, lst) for c, lst in g["d3"].items()]
+        seg = None
+        for kind, lst in units:
+            if cur is None or (cur["terms"] and len(cur["terms"]) + len(lst) > maxb):
+                if seg is not None:
+                    seg["last"] = False
+                cur = new_block()
+                seg = None
+            if seg is None:
+                seg = {"a": a, "b": b, "first": not any(s_["a"] == a and s_["b"] == b
+                                                        for b_ in blocks for s_ in b_.get("segs", [])),
+                       "last": True, "d2": [], "d3": []}
+                cur["segs"].append(seg)
+            if kind == "d2":
+                seg["d2"] += lst
+            else:
+                seg["d3"].append((kind, lst))
             cur["terms"] += [t for t, _ in lst]
-        cur["last"] = True
-        blocks.append(cur)
     return blocks
 
 
@@ -714,7 +733,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    NB = 64                                 # nodes per workgroup (fwd / grad-x), one per lane
+    NB = 64 * SC_NT                         # nodes per workgroup (fwd / grad-x), one per lane
+    NTH = 256 * SC_NT                       # threads per workgroup (fwd / grad-x)
 
     # Staging between the mul-major rows and the quad tile.  A quad owns, per node and l-block,
     # one run of 4*d floats (d float4, 16-B aligned), so a tile of nb nodes is nb * D float4:
@@ -731,13 +751,13 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             expr = v if expr is None else f"({j} >= {st4} ? {v} : {expr})"
         return expr
 
-    def stage_in(src, tile, lay, nb=64):
+    def stage_in(src, tile, lay, nb=64, nth=256):
         n4 = lay.QD // 4
         tot = nb * n4
-        it_n = -(-tot // 256)
+        it_n = -(-tot // nth)
         out = ["  { int cqo_ = cq; asm volatile(\"\" : \"+s\"(cqo_));"]
         for it in range(it_n):
-            out.append(f"    const int i{it} = min((int)threadIdx.x + {256 * it}, {tot - 1}), "
+            out.append(f"    const int i{it} = min((int)threadIdx.x + {nth * it}, {tot - 1}), "
                        f"nl{it} = i{it} / {n4}, j{it} = i{it} - nl{it} * {n4};")
             out.append(f"    const float4 v{it} = *reinterpret_cast<const float4*>({src} + "
                        f"(size_t)min(n0 + nl{it}, n_nodes - 1) * {lay.row} + {_gofs(lay, f'j{it}')});")
@@ -750,20 +770,20 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         out.append("  }")
         return out
 
-    def stage_out(dst, tile, lay, nb=64):
+    def stage_out(dst, tile, lay, nb=64, nth=256):
         n4 = lay.QD // 4
         tot = nb * n4
         out = ["  { int cqo_ = cq; asm volatile(\"\" : \"+s\"(cqo_));"]
-        for it in range(-(-tot // 256)):
-            out.append(f"    {{ const int i_ = (int)threadIdx.x + {256 * it}, nl_ = i_ / {n4}, j_ = i_ - nl_ * {n4};")
-            guard = f"i_ < {tot} && " if 256 * (it + 1) > tot else ""
+        for it in range(-(-tot // nth)):
+            out.append(f"    {{ const int i_ = (int)threadIdx.x + {nth * it}, nl_ = i_ / {n4}, j_ = i_ - nl_ * {n4};")
+            guard = f"i_ < {tot} && " if nth * (it + 1) > tot else ""
             out.append(f"      if ({guard}n0 + nl_ < n_nodes) {{ const float* t_ = {tile} + nl_ * {TP} + 4 * j_; "
                        f"*reinterpret_cast<float4*>({dst} + (size_t)(n0 + nl_) * {lay.row} + {_gofs(lay, 'j_')}) = "
                        "make_float4(t_[0], t_[1], t_[2], t_[3]); } }")
         out.append("  }")
         return out
 
-    def cm_store(dst, tile, lay, nb, ind="  "):
+    def cm_store(dst, tile, lay, nb, ind="  ", nth=256):
         """dst[(c * D + a) * n_nodes + n] = component a of channel c of node n, from a staged
         tile of nb nodes x the quad's 4 channels (coalesced nb-float runs per (c, a))"""
         dd = lay.D
@@ -782,7 +802,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         # values were hoisted to the kernel top and spilled SGPRs in grad-x)
         out = ["{ int tid_ = threadIdx.x; asm volatile(\"\" : \"+v\"(tid_));",
                "#pragma unroll 1",
-               f"  for (int i_ = tid_; i_ < {tot}; i_ += 256) {{",
+               f"  for (int i_ = tid_; i_ < {tot}; i_ += {nth}) {{",
                f"    const int row_ = i_ >> {sh}, nl_ = i_ & {nb - 1};",
                f"    const int cl_ = row_ / {dd}, a_ = row_ - cl_ * {dd};",
                f"    if (n0 + nl_ < n_nodes) {dst}[(size_t)((cq * {Q} + cl_) * {dd} + a_) * n_nodes + n0 + nl_] = "
@@ -808,30 +828,32 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # owns a 16*d-byte run of each 128*d-byte l-block) are fetched from HBM once, into that
     # XCD's L2, and its partial-line stores merge there
     NQ = MUL // Q
-    tile_map = ["  const int xcd = blockIdx.x & 7, rest_ = blockIdx.x >> 3;",
+    def tile_map(nb):
+        return ["  const int xcd = blockIdx.x & 7, rest_ = blockIdx.x >> 3;",
                 f"  const int cq = rest_ % {NQ};",
-                f"  const int n0 = ((rest_ / {NQ}) * 8 + xcd) * 64;",
+                f"  const int n0 = ((rest_ / {NQ}) * 8 + xcd) * {nb};",
                 "  if (n0 >= n_nodes) return;   // uniform per workgroup (tile count padded to 8)"]
-    head = tile_map + [
+    nrow = "lane" if SC_NT == 1 else "((wv >> 2) * 64 + lane)"   # this lane's node row in the tile
+    head = tile_map(NB) + [
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
             f"  const int cl = __builtin_amdgcn_readfirstlane(wv & {Q - 1});",
             f"  const float* __restrict__ cf = coef + (size_t)c * {nt};"]
 
     # ---------------- forward ----------------
-    L.append(f"__global__ __launch_bounds__(256) void sc_fwd_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[{NB} * {TP}];")
     L += head
-    L += stage_in("x", "tile", lin, NB)
+    L += stage_in("x", "tile", lin, NB, NTH)
     L.append("  __syncthreads();")
-    L.append(f"  float* __restrict__ tr = tile + lane * {TP};")
+    L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
     for a in range(D):
         L.append(f"  float x{a} = tr[{lq(lin, a, 'cl')}];")
     for q in range(Dout):
         L.append(f"  float o{q} = 0.0f;")
-    blocks = sc_blocks(plan)
+    blocks = sc_blocks(plan, SC_BLOCK)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
     for b0 in blocks[:SC_PFD_FWD]:
         for t in b0["terms"]:
@@ -845,31 +867,31 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
                 L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
-        else:
-            a, b = blk["a"], blk["b"]
+        for sg in blk.get("segs", []):
+            a, b = sg["a"], sg["b"]
             pv = f"p{a}_{b}"
-            if blk["first"]:
+            if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b};")
-            for t, q in blk["d2"]:
+            for t, q in sg["d2"]:
                 L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
-            for cc, lst in blk["d3"]:
+            for cc, lst in sg["d3"]:
                 L.append(f"  {{ const float m = {pv} * x{cc};")
                 for t, q in lst:
                     L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
                 L.append("  }")
-            if not blk["last"]:
+            if not sg["last"]:
                 carry = [pv]
         L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for q in range(Dout):
         L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
     L.append("  __syncthreads();")
-    L += stage_out("out", "tile", lout, NB)
+    L += stage_out("out", "tile", lout, NB, NTH)
     L.append("}")
 
 
     # ---------------- backward w.r.t. x ----------------
-    L.append(f"__global__ __launch_bounds__(256) void sc_bwd_x_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
     L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
@@ -878,20 +900,20 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
     L.append(f"  __shared__ float tx[{NB} * {TP}];")
     L += head
-    L += stage_in("x", "tx", lin, NB)
+    L += stage_in("x", "tx", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (xt) {")
-    L += cm_store("xt", "tx", lin, NB, "    ")
+    L += cm_store("xt", "tx", lin, NB, "    ", NTH)
     L.append("  }")
-    L.append(f"  float* __restrict__ xr = tx + lane * {TP};")
+    L.append(f"  float* __restrict__ xr = tx + {nrow} * {TP};")
     for a in range(D):
         L.append(f"  float x{a} = xr[{lq(lin, a, 'cl')}];")
         L.append(f"  float d{a} = 0.0f;")
     L.append("  __syncthreads();")
-    L += stage_in("gout", "tx", lout, NB)
+    L += stage_in("gout", "tx", lout, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (gt) {")
-    L += cm_store("gt", "tx", lout, NB, "    ")
+    L += cm_store("gt", "tx", lout, NB, "    ", NTH)
     L.append("  }")
     for q in range(Dout):
         L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
@@ -908,19 +930,19 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
                 L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
-        else:
-            a, b = blk["a"], blk["b"]
+        for sg in blk.get("segs", []):
+            a, b = sg["a"], sg["b"]
             pv, sv = f"p{a}_{b}", f"s{a}_{b}"
-            if blk["first"]:
+            if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
-            for t, q in blk["d2"]:
+            for t, q in sg["d2"]:
                 L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
-            for cc, lst in blk["d3"]:
+            for cc, lst in sg["d3"]:
                 L.append("  { float s = 0.0f;")
                 for t, q in lst:
                     L.append(f"    s = fmaf(c{t}, g{q}, s);")
                 L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
-            if blk["last"]:
+            if sg["last"]:
                 L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
             else:
                 carry = [pv, sv]
@@ -929,7 +951,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     for a in range(D):
         L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
     L.append("  __syncthreads();")
-    L += stage_out("gx", "tx", lin, NB)
+    L += stage_out("gx", "tx", lin, NB, NTH)
     L.append("}")
 
     # ---------------- mul-major -> channel-major transpose ----------------
@@ -939,7 +961,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"__global__ __launch_bounds__(256) void {kname}(")
         L.append("    const float* __restrict__ x, int n_nodes, float* __restrict__ xt) {")
         L.append(f"  __shared__ float tile[64 * {TP}];")
-        L.extend(tile_map)
+        L.extend(tile_map(64))
         L.extend(stage_in("x", "tile", lay))
         L.append("  __syncthreads();")
         L.extend(cm_store("xt", "tile", lay, 64))
@@ -1070,7 +1092,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nbc=NBC,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nbc=NBC, nb=NB, nth=NTH,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -1110,7 +1132,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nbc"]}}},')
+                     f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")
