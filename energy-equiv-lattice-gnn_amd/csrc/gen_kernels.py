@@ -38,11 +38,13 @@ TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
-# computed, forward / grad-x (r03m: grad-x 0.44 ms at 2; at 3 it spills SGPRs into VGPR lanes
-# once the staging is rewritten, 0.60 ms; the forward spills SGPRs at 2+)
+# computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
+# 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
+# 1 ahead, it spills SGPRs beyond)
 SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
-SC_BLOCK = int(os.environ.get("EELG_SC_BLOCK", "32"))     # terms per coefficient block
-SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "2"))
+SC_BLOCK_FWD = int(os.environ.get("EELG_SC_BLOCK_FWD", "32"))
+SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "1"))
+SC_BLOCK_BWD = int(os.environ.get("EELG_SC_BLOCK_BWD", "64"))
 # fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
 # consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
 SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
@@ -853,7 +855,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  float x{a} = tr[{lq(lin, a, 'cl')}];")
     for q in range(Dout):
         L.append(f"  float o{q} = 0.0f;")
-    blocks = sc_blocks(plan, SC_BLOCK)
+    blocks = sc_blocks(plan, SC_BLOCK_FWD)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
     for b0 in blocks[:SC_PFD_FWD]:
         for t in b0["terms"]:
@@ -918,6 +920,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     for q in range(Dout):
         L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
+    blocks = sc_blocks(plan, SC_BLOCK_BWD)
     for b0 in blocks[:SC_PFD_BWD]:
         for t in b0["terms"]:
             L.append(f"  float c{t} = cf[{t}];")
