@@ -36,7 +36,9 @@ MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
-TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
+TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))
+# tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
+TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))   # r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
@@ -475,12 +477,20 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
                                                     f"{p.out_off} + u * {d3}")]
             out.append(f"      float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
+        PF = TP_BWD_PFD
+        regs_of = {}
+        for pj in range(1, min(PF, len(grp))):   # paths 1 .. PF-1 issued up front
+            code, regs_of[pj] = pref(grp[pj])
+            L += code
         for pi, p in enumerate(grp):
             d3 = 2 * p.l3 + 1
             d1 = 2 * p.l1 + 1
-            if pi + 1 < len(grp):            # next path's loads in flight during this one
-                code, nxt_regs = pref(grp[pi + 1])
+            if pi + PF < len(grp):           # path pi + PF's loads in flight during this one
+                code, regs_of[pi + PF] = pref(grp[pi + PF])
                 L += code
+            if pi + 1 < len(grp):
+                # only the next path must have landed after this one; later paths stay in flight
+                nxt_regs = regs_of[pi + 1]
             elif EPH > 1:                    # next edge's loads in flight during the last path
                 L += ["  " + ln for ln in edge_loads("n", "sn", "rn", "en")]
                 nxt_regs = ["n" + v for v in xs_ + ys_ + g0_]
