@@ -36,9 +36,10 @@ MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
-TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))
+TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
-TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))   # r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
+# (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
+TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
