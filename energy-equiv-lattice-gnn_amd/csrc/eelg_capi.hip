@@ -435,11 +435,12 @@ static const eelg_tp_cfg* tp_cfg(int cfg) {
   return &t[cfg];
 }
 
-// node tiles of 8 * nph receivers (4 waves x 2 half-waves); the tile count is rounded up to a
-// multiple of 8 so every tile's ngroups blocks land on one XCD, which takes a contiguous range
-// of tiles (see gen_kernels.py); surplus blocks exit
+// node tiles of 2 * fwpb * nph receivers (fwpb waves x 2 half-waves); the tile count is rounded
+// up to a multiple of 8 so every tile's ngroups blocks land on one XCD, which takes a contiguous
+// range of tiles (see gen_kernels.py); surplus blocks exit
 static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes) {
-  const int tiles = (n_nodes + 8 * c.nph - 1) / (8 * c.nph);
+  const int tn = 2 * c.fwpb * c.nph;
+  const int tiles = (n_nodes + tn - 1) / tn;
   return dim3(((tiles + 7) / 8) * 8 * c.ngroups);
 }
 
@@ -448,7 +449,7 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(64 * c->fwpb), 0, (hipStream_t)stream, x,
                      sh, w, sender, rowptr, n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");
 }
@@ -458,7 +459,7 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(64 * c->fwpb), 0, (hipStream_t)stream,
                      x, sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
                      agg);
   return check_launch("tp_fwd_bf16");

@@ -31,6 +31,7 @@ struct eelg_tp_cfg {
   int din, dmid, wn, nsh, ngroups, npaths, lmax, nbgroups;
   int nph;   // tp_fwd: receivers per half-wave
   int beph;  // tp_bwd: edges per half-wave
+  int fwpb;  // tp_fwd: waves per workgroup
   uint64_t sig;
   eelg_tp_fwd_fn fwd;
   eelg_tp_bwd_fn bwd;

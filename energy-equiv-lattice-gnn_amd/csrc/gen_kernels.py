@@ -36,6 +36,10 @@ MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
+# tp_fwd waves per workgroup (a node tile = 2 x TP_FWD_WPB x TP_NPH receivers; one-wave
+# workgroups refill a freed wave slot at once: r03z kbench 0.505 vs 0.520 ms at 4, 0.518 at 2;
+# in the step 0.438 vs 0.446 ms)
+TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
@@ -56,6 +60,9 @@ SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
 SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
 SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
+# coefficient gradient: term groups clustered by shared operands (coef_groups) instead of runs
+# of the term order
+SC_COEF_CLUSTER = int(os.environ.get("EELG_SC_COEF_CLUSTER", "1"))
 # Variants built, measured slower and removed (DESIGN.md section 3 records the numbers): packed
 # channel-pair TP forward, 2x-unrolled TP edge loop, shared-coupling (M in LDS) and cooperative
 # TP forwards, two nodes / two channels per lane in the contraction, mul-major coefficient
@@ -299,7 +306,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
-    L.append(f"__global__ __launch_bounds__(256) void tp_fwd_{name}{sfx}(")
+    L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
@@ -308,10 +315,11 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the x
     # rows of a lattice are gathered by one XCD (its L2) rather than by all eight (r03h: 1828
     # -> 1865 graphs/s together with the 64-accumulator groups)
-    L.append(f"  const int ntl = (n_nodes + {8 * TP_NPH - 1}) / {8 * TP_NPH}, tpx = (ntl + 7) >> 3;")
+    TN = 2 * TP_FWD_WPB * TP_NPH          # receivers per node tile (one workgroup)
+    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
     L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
     L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
-    L.append(f"  const int n0 = ((tile * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
+    L.append(f"  const int n0 = ((tile * {TP_FWD_WPB} + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
     L.append("  if (n0 >= n_nodes) return;")
     L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
     L.append("  switch (grp) {")
@@ -619,7 +627,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  }")
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
-                npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, sig=fnv1a64(tp_signature(node, sh, target)))
+                npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, fwpb=TP_FWD_WPB, sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
 
@@ -684,6 +692,81 @@ def sc_blocks(plan, maxb: int = 32) -> List[Dict]:
                 seg["d3"].append((kind, lst))
             cur["terms"] += [t for t, _ in lst]
     return blocks
+
+
+def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> List[List[int]]:
+    """Term groups of the coefficient gradient, clustered so that a group reads few operands.
+
+    A lane (one node) of a group loads every x_a / g_q the group's terms use from LDS once per
+    64-node sub-tile, and the LDS operand reads, not the VALU, bounded the kernel when groups
+    were runs of the term order (35 operands per 59 terms: 16 waves x 35 x 2 LDS cycles per CU
+    against 4 waves x 85 x 2 VALU cycles per SIMD).  Greedy clustering: a group grows by the
+    term adding the fewest ``lds_w`` x new operands + new products (x_a x_b, x_a x_b x_c), so
+    the operand union drops to ~18 and the VALU count (one FMA per term + the shared products)
+    becomes the bound.  The groups are then dealt to the waves longest-first (each wave takes
+    n_groups / n_waves of them; a workgroup holds its CU until its slowest wave ends), and
+    returned in launch order: group k * n_waves + w belongs to wave w."""
+    import numpy as np
+    terms = plan.terms
+    nt = len(terms)
+    opm = np.zeros(nt, dtype=np.uint64)
+    abid = np.full(nt, -1, dtype=np.int64)
+    abcid = np.full(nt, -1, dtype=np.int64)
+    ab_ix, abc_ix = {}, {}
+    nx = 1 + max(max(a, b, c) for _, (a, b, c), _ in terms)
+    for t, (nu, (a, b, c), q) in enumerate(terms):
+        m = (1 << a) | (1 << (nx + q))
+        if nu >= 2:
+            m |= 1 << b
+            abid[t] = ab_ix.setdefault((a, b), len(ab_ix))
+        if nu >= 3:
+            m |= 1 << c
+            abcid[t] = abc_ix.setdefault((a, b, c), len(abc_ix))
+        opm[t] = m
+    assert 2 * nx <= 64
+    left = np.ones(nt, dtype=bool)
+    groups = []
+    BIG = np.int64(1 << 40)
+    while left.any():
+        g = [int(np.argmax(left))]
+        left[g[0]] = False
+        um = opm[g[0]]
+        hab = np.zeros(len(ab_ix) + 1, dtype=bool)
+        habc = np.zeros(len(abc_ix) + 1, dtype=bool)
+        hab[abid[g[0]]] = True
+        habc[abcid[g[0]]] = True
+        while len(g) < jg and left.any():
+            new_ops = np.bitwise_count(opm & ~um).astype(np.int64)
+            cost = (lds_w * new_ops + (~hab[abid] & (abid >= 0)) + (~habc[abcid] & (abcid >= 0)))
+            cost = np.where(left, cost, BIG)
+            t = int(np.argmin(cost))
+            g.append(t)
+            left[t] = False
+            um |= opm[t]
+            hab[abid[t]] = True
+            habc[abcid[t]] = True
+        groups.append(g)
+    assert len(groups) <= n_groups, (len(groups), n_groups)
+
+    def cost(g):
+        ops, prods = set(), set()
+        for t in g:
+            nu, (a, b, c), q = terms[t]
+            ops |= {("x", a), ("g", q)} | ({("x", b)} if nu >= 2 else set()) | ({("x", c)} if nu >= 3 else set())
+            prods |= ({(a, b)} if nu >= 2 else set()) | ({(a, b, c)} if nu >= 3 else set())
+        return max(4 * len(ops), len(prods) + len(g))
+    per = n_groups // n_waves
+    load = [0] * n_waves
+    slots: List[List[List[int]]] = [[] for _ in range(n_waves)]
+    for g in sorted(groups, key=cost, reverse=True):
+        w = min((w for w in range(n_waves) if len(slots[w]) < per), key=lambda w: load[w])
+        slots[w].append(g)
+        load[w] += cost(g)
+    out = []
+    for k in range(per):
+        for w in range(n_waves):
+            out.append(slots[w][k] if k < len(slots[w]) else [])
+    return out
 
 
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
@@ -999,11 +1082,20 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     gpw = -(-nt // (WV * SC_COEF_MAXJG))      # term groups per wave
     JG = -(-nt // (WV * gpw))                 # terms per group (<= 64)
     assert JG <= 64 and NCB % 64 == 0
-    groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
+    if SC_COEF_CLUSTER:
+        groups = coef_groups(plan, WV, JG, WV * gpw)
+    else:
+        groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
+    # lane j of group g ends with the sum of term perm[g * 64 + j] (-1: no term)
+    perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
     nsub = NCB // 64
     NC4 = NCB // 4
-    L.append(f"// coefficient gradient: {len(groups)} term groups of <= {JG} terms, {gpw} per wave;")
+    L.append(f"// coefficient gradient: {sum(1 for g in groups if g)} term groups of <= {JG} terms, {gpw} per wave;")
     L.append(f"// one workgroup = one channel x {NCB} LDS-resident nodes")
+    L.append(f"__device__ const short sc_coef_perm_{name}[{len(perm)}] = {{")
+    for k in range(0, len(perm), 32):
+        L.append("  " + ", ".join(str(v) for v in perm[k: k + 32]) + ",")
+    L.append("};")
     L.append(f"__global__ __launch_bounds__({64 * WV}) void sc_bwd_coef_{name}(")
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int chunk,")
     L.append("    float* __restrict__ part) {")
@@ -1059,6 +1151,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
     L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
+        if not grp:
+            continue
         L.append(f"    case {gi}: {{")
         need_x, need_g = set(), set()
         for t in grp:
@@ -1077,8 +1171,12 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             L.append(f"        const float x{a} = sx[{a * SXS} + o];")
         for q in sorted(need_g):
             L.append(f"        const float g{q} = sg[{q * SXS} + o];")
-        cur = None
-        for jj, t in enumerate(grp):
+        # accumulator jj belongs to term grp[jj]; walk the terms by (a, b, c) so each pair
+        # product and each triple product is formed once per group
+        order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
+        cur, curc = None, None
+        for jj in order:
+            t = grp[jj]
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
                 L.append(f"        acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
@@ -1088,11 +1186,14 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                     L.append("        }")
                     L.append("        " + cpin)
                 L.append(f"        {{ const float p = x{a} * x{b};")
-                cur = (a, b)
+                cur, curc = (a, b), None
             if nu == 2:
                 L.append(f"          acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
             else:
-                L.append(f"          acc[{jj}] = fmaf(p * x{cc}, g{q}, acc[{jj}]);")
+                if curc != cc:
+                    L.append(f"          const float m{cc} = p * x{cc};")
+                    curc = cc
+                L.append(f"          acc[{jj}] = fmaf(m{cc}, g{q}, acc[{jj}]);")
         if cur is not None:
             L.append("        }")
         L.append("        " + cpin)
@@ -1101,8 +1202,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    default: break;")
     L.append("    }")
     L.append("    eelg_lane_reduce64(acc);")
-    L.append(f"    const int t = jg * {JG} + lane;")
-    L.append(f"    if (jg < {len(groups)} && lane < {JG} && t < {nt}) dst[t] = acc[0];")
+    L.append(f"    const int t = jg < {len(groups)} ? sc_coef_perm_{name}[jg * 64 + lane] : -1;")
+    L.append("    if (t >= 0) dst[t] = acc[0];")
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
@@ -1139,7 +1240,7 @@ def main(outdir: str) -> None:
     for name, i in tp_table:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
-                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
+                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
                      f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
