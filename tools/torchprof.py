@@ -45,6 +45,8 @@ def main():
         torch.cuda.synchronize()
     ka = prof.key_averages()
     print(ka.table(sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60))
+    # host side: where the Python thread spends its time enqueueing the step
+    print(ka.table(sort_by="self_cpu_time_total", row_limit=40, max_name_column_width=60))
     print(prof.key_averages(group_by_stack_n=4).table(sort_by="self_cuda_time_total", row_limit=30,
                                                       max_name_column_width=40, max_src_column_width=90))
 
