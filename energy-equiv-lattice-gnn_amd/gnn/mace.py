@@ -111,6 +111,7 @@ class SymmetricContraction(torch.nn.Module):
         self._cfg = None
         self._coupling, self._ls = coupling, ls
         self._u_loaded = {}          # (l, nu) -> U adopted from a loaded state_dict (CPU f32)
+        self._ahead = None           # (coef, event, stream) issued by coefficients_ahead
         self._register_state_dict_hook(SymmetricContraction._emit_reference_U)
 
     # -- reference checkpoints (gnn/mace.py:198-205: U_matrix_{nu} buffers per Contraction) --
@@ -216,9 +217,27 @@ class SymmetricContraction(torch.nn.Module):
         # backward -- and the coefficient-gradient kernel launched there by the contraction's
         # backward -- overlaps the rest of the backward on the main stream
         main = torch.cuda.current_stream(x.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            coef = self.coefficients()
-        main.wait_stream(side)
+        ahead, self._ahead = self._ahead, None
+        if ahead is not None and ahead[2] is side:
+            coef, ev = ahead[0], ahead[1]
+            main.wait_event(ev)
+        else:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                coef = self.coefficients()
+            main.wait_stream(side)
         coef.record_stream(main)
         return ops.symmetric_contraction(x, coef, idx, info, self.mul, side=side)
+
+    def coefficients_ahead(self, side) -> None:
+        """Issue the coefficient chain (weight matrix -> U_sym SpMM) on the side stream now and
+        keep (coef, event) for this module's next forward.  The model calls it for every layer
+        at the start of its forward (the coefficients depend on the weights only), so each
+        layer's main stream waits on work finished long before, instead of a main -> side ->
+        main round trip at the layer (two cross-stream waits of ~20 us each on the critical
+        path).  The caller orders ``side`` after the main stream's last weight update."""
+        with torch.cuda.stream(side):
+            coef = self.coefficients()
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self._ahead = (coef, ev, side)

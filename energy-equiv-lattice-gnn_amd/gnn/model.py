@@ -42,6 +42,8 @@ def storage_dtype(params: Namespace) -> torch.dtype:
 
 # every layer's radial MLP done before layer 1 starts (they overlap layer 0 only)
 RADIAL_AHEAD_OF_LAYER1 = os.environ.get("EELG_RADIAL_BEFORE_L1", "1") != "0"
+# every layer's contraction coefficients issued at the start of the forward (GNN_Head._coefficients_ahead)
+COEF_AHEAD = os.environ.get("EELG_COEF_AHEAD", "1") != "0"
 
 
 class GNN_Head(torch.nn.Module):  # noqa: N801
@@ -103,9 +105,22 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
             w.record_stream(main)        # allocator: w is also used on the main stream
         return ws, evs
 
+    def _coefficients_ahead(self, device) -> None:
+        """Every layer's contraction coefficients (``coef = U_sym W``) depend on the weights
+        only: issue them all up front on the coefficient side stream (after the main stream's
+        last weight update), so no layer waits on a fresh main -> side -> main round trip."""
+        if not (ops.OVERLAP and COEF_AHEAD and device.type == "cuda"):
+            return
+        main = torch.cuda.current_stream(device)
+        side = ops.side_stream(device, 1)
+        side.wait_stream(main)
+        for layer in self.layers:
+            layer.product.symmetric_contractions.coefficients_ahead(side)
+
     def forward(self, edge_index, node_ft, edge_sh, edge_feats, batch_idx, num_graphs: int):
         csr, edge_sh, edge_feats = as_csr(edge_index, node_ft.shape[0], edge_sh, edge_feats)
         ws, evs = self._radial_weights_ahead(edge_feats)
+        self._coefficients_ahead(node_ft.device)
 
         def run(i, h, residual=None):
             if evs[i] is not None:
