@@ -40,6 +40,11 @@ TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 # workgroups refill a freed wave slot at once: r03z kbench 0.505 vs 0.520 ms at 4, 0.518 at 2;
 # in the step 0.438 vs 0.446 ms)
 TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
+# tp_fwd: the next edge's x / SH / weight rows prefetched into LDS by LDS-DMA (global_load_lds)
+# instead of a second register set (fp32 storage only)
+TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "0"))
+# LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
+TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
@@ -271,6 +276,362 @@ def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
     return out
 
 
+def _glds_chunks(groups, nshp, node_off):
+    """Per path group: the 16-B chunk list of one half-wave's rows for one edge (x blocks of
+    x[sender], the SH row, the group's weight slices) and the image float offsets."""
+    glist = []
+    for grp in groups:
+        need_l1 = sorted({p.l1 for p in grp})
+        need_l2 = sorted({p.l2 for p in grp})
+        chunks, fo_x, fo_w = [], {}, {}
+        for l in need_l1:
+            fo_x[l] = 4 * len(chunks)
+            chunks += [(0, 4 * node_off[l] + 16 * cc) for cc in range(8 * (2 * l + 1))]
+        fo_sh = 4 * len(chunks)
+        chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
+        for p in grp:
+            fo_w[p.slot] = 4 * len(chunks)
+            chunks += [(2, 4 * p.slot * MUL + 16 * cc) for cc in range(8)]
+        glist.append((need_l1, need_l2, chunks, fo_x, fo_sh, fo_w))
+    return glist
+
+
+def _glds_desc(chunks, nj) -> List[str]:
+    """per-lane chunk descriptors (loop-invariant): chunk 64 j + lane = (row kind, byte offset)"""
+    out = []
+    for j in range(nj):
+        runs = []
+        for c in range(64 * j, min(64 * j + 64, len(chunks))):
+            k, o = chunks[c]
+            if runs and runs[-1][2] == k and runs[-1][3] + 16 * (c - runs[-1][0]) == o and runs[-1][1] == c:
+                runs[-1][1] = c + 1
+            else:
+                runs.append([c, c + 1, k, o])
+        kexpr, oexpr = "1", "0"             # past the list: chunk 0 of the SH row (discarded)
+        for a, b, k, o in reversed(runs):
+            kexpr = f"(c_ < {b} ? {k} : {kexpr})"
+            oexpr = f"(c_ < {b} ? {o} + 16 * (c_ - {a}) : {oexpr})"
+        out.append(f"    int kd{j}, of{j}; {{ const int c_ = {64 * j} + lane; kd{j} = {kexpr}; of{j} = {oexpr}; }}")
+    return out
+
+
+def _glds_compute(grp, cur, accs) -> List[str]:
+    """edge e's contribution of one path group, from the registers in ``cur``"""
+    L = []
+    cpin = pin(accs + cur)
+    xn = lambda p, i: f"x{p.l1}_{i}"  # noqa: E731
+    yn = lambda p, j: f"y{p.l2 * p.l2 + j}"  # noqa: E731
+    for p in grp:
+        d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
+        L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+        L.append(f"        const float wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
+        fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
+        if fold[1] == "none":
+            _emit_t(p, xn, yn, "t", L, "        ")
+            for k in range(d3):
+                L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+        else:
+            if fold[1] == "x":
+                for i in range(d1):
+                    L.append(f"        const float xw{i} = {xn(p, i)} * wp;")
+                xf, yf = (lambda p, i: f"xw{i}"), yn
+            else:
+                for j in range(d2):
+                    L.append(f"        const float yw{j} = {yn(p, j)} * wp;")
+                xf, yf = xn, (lambda p, j: f"yw{j}")
+            _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", L, "        ")
+        L.append("      }")
+        L.append("      " + cpin)
+    return L
+
+
+def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]:
+    """tp_fwd with the rows of edges e+1 AND e+2 in flight by LDS-DMA (two LDS images per
+    half-wave) while edge e computes.  The per-half-wave stream state (edge, receiver, the
+    rowptr entries, the sender indices) is wave-uniform per half and kept in SGPRs with scalar
+    loads, so the loop issues no vector load besides the LDS-DMA ones and a counted
+    ``s_waitcnt vmcnt(N)`` (N = the LDS-DMA instructions of one edge) retires edge e+1's rows
+    while edge e+2's stay in flight.  Stores of a half-wave's aggregates are exec-masked to
+    its lanes."""
+    WPB = TP_FWD_WPB
+    TN = 2 * WPB * TP_NPH
+    ng = len(groups)
+    glist = _glds_chunks(groups, nshp, node_off)
+    NJ = max(-(-len(g[2]) // 64) for g in glist)
+    NI = NJ * 64
+    L: List[str] = []
+    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_FWD_WPE})))" if TP_FWD_WPE else ""
+    L.append(f"__global__ __launch_bounds__({64 * WPB}){wpe} void tp_fwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
+    L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5;")
+    L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
+    L.append("  if (nw0 >= n_nodes) return;   // uniform per wave; a half past the end gets no receivers")
+    L.append("  float4* __restrict__ ib = &img_[wv][0][0][0];")
+    L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)ib);")
+    for h in (0, 1):
+        L.append(f"  const int n0_{h} = min(nw0 + {h * TP_NPH}, n_nodes), n1_{h} = min(n0_{h} + {TP_NPH}, n_nodes);")
+        L.append(f"  int e_{h} = rowptr[n0_{h}];")
+        L.append(f"  const int eend_{h} = rowptr[n1_{h}];")
+        L.append(f"  int node_{h} = n0_{h}, nend_{h} = rowptr[min(n0_{h} + 1, n1_{h})], "
+                 f"nend2_{h} = rowptr[min(n0_{h} + 2, n1_{h})];")
+    L.append("  switch (grp) {")
+    for gi, grp in enumerate(groups):
+        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
+        nj = -(-len(chunks) // 64)
+        L.append(f"  case {gi}: {{ // {len(chunks)} chunks of 16 B per half-wave and edge")
+        L += _glds_desc(chunks, nj)
+
+        def issue(buf, ahead):
+            out = ["    {"]
+            for h in (0, 1):
+                out.append(f"      {{ const int ee_ = e_{h} + {ahead} < eend_{h} ? e_{h} + {ahead} : 0;")
+                out.append(f"        const int ss_ = e_{h} + {ahead} < eend_{h} ? sender[ee_] : 0;")
+                out.append(f"        const char* xb = reinterpret_cast<const char*>(x + (size_t)ss_ * {din});")
+                out.append(f"        const char* shb = reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp});")
+                out.append(f"        const char* wb = reinterpret_cast<const char*>(w + (size_t)ee_ * {wn});")
+                out.append(f"        float4* dst = ib + ({buf}) * {2 * NI} + {h * NI};")
+                for j in range(nj):
+                    out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
+                               f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
+                               f"(__attribute__((address_space(3))) void*)(dst + {64 * j}), 16, 0, 0);")
+                out.append("      }")
+            out.append("    }")
+            return out
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
+               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+               + [f"w{p.slot}" for p in grp])
+        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
+        L += issue("0", 0)
+        L += issue("1", 1)
+        L.append("    int b = 0;")
+        L.append("    for (;;) {")
+        # edge e's rows: everything but the last edge's LDS-DMA instructions has landed
+        L.append(f'      asm volatile("s_waitcnt vmcnt({2 * nj})" ::: "memory");')
+        # the LDS reads are inline asm: hipcc would otherwise order every LDS read after ALL
+        # outstanding LDS-DMA (a vmcnt(0): it cannot tell the image being read from the one
+        # being filled), which would retire edge e+2's rows too
+        L.append(f"      const unsigned imb = lds0 + b * {2 * NI * 16} + hf * {NI * 16};")
+        L.append("      float " + ", ".join(cur) + ";")
+        tdecl = [f"tx{l}_{i}" for l in need_l1 for i in range(0, 2 * l, 2)]
+        if tdecl:
+            L.append("      eelg_f2r " + ", ".join(tdecl) + ";")
+        need_y0 = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
+        L.append("      eelg_f4r " + ", ".join(f"ty{blk}" for blk in sorted({j // 4 for j in need_y0})) + ";")
+        # asm outputs are taken as ready when the statement ends: every destination register
+        # (vector temporaries included) is threaded through the lgkmcnt wait before any use
+        live, after = [], []
+        for l in need_l1:
+            d = 2 * l + 1
+            L.append(f"      {{ const unsigned xa = imb + 4 * ({fo_x[l]} + u * {d});")
+            i = 0
+            while i < d:
+                if i + 1 < d:
+                    L.append(f"        asm volatile(\"ds_read2_b32 %0, %1 offset0:{i} offset1:{i + 1}\" : \"=v\"(tx{l}_{i}) : \"v\"(xa));")
+                    live.append(f"tx{l}_{i}")
+                    after.append(f"x{l}_{i} = tx{l}_{i}[0]; x{l}_{i + 1} = tx{l}_{i}[1];")
+                    i += 2
+                else:
+                    L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * i}\" : \"=v\"(x{l}_{i}) : \"v\"(xa));")
+                    live.append(f"x{l}_{i}")
+                    i += 1
+            L.append("      }")
+        need_y = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
+        for blk in sorted({j // 4 for j in need_y}):
+            L.append(f"      asm volatile(\"ds_read_b128 %0, %1 offset:{4 * fo_sh + 16 * blk}\" : \"=v\"(ty{blk}) : \"v\"(imb));")
+            live.append(f"ty{blk}")
+            after.append(" ".join(f"y{j} = ty{blk}[{j - 4 * blk}];" for j in need_y if j // 4 == blk))
+        L.append("      { const unsigned wa = imb + 4 * u;")
+        for p in grp:
+            L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(w{p.slot}) : \"v\"(wa));")
+            live.append(f"w{p.slot}")
+        L.append("      }")
+        for k in range(0, len(live), 24):
+            ops = ", ".join(f'"+v"({v})' for v in live[k: k + 24])
+            L.append(f'      asm volatile("s_waitcnt lgkmcnt(0)" : {ops} : : "memory");')
+        L += ["      " + a_ for a_ in after]
+        L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
+        for h in (0, 1):
+            L.append(f"      while (node_{h} < n1_{h} && nend_{h} == e_{h}) {{   // uniform")
+            L.append(f"        if (hf == {h}) {{")
+            L.append(f"          float* __restrict__ o = agg + (size_t)node_{h} * {dmid};")
+            for p in grp:
+                d3 = 2 * p.l3 + 1
+                L.extend("          " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                             f"{p.out_off} + u * {d3}"))
+            L.append("          " + " ".join(f"{a} = 0.0f;" for a in accs))
+            L.append("        }")
+            L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
+            L.append("      }")
+        L.append("      if (e_0 >= eend_0 && e_1 >= eend_1) break;")
+        L += ["  " + ln for ln in issue("b", 2)]
+        L += _glds_compute(grp, cur, accs)
+        L.append("      ++e_0; ++e_1; b ^= 1;")
+        L.append("    }")
+        L.append('    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the wave')
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
+def _emit_tp_fwd_glds(name, groups, din, nshp, dmid, wn, node_off) -> List[str]:
+    """tp_fwd with the next edge's rows prefetched into LDS by LDS-DMA.
+
+    Same mapping and arithmetic as the register-pipelined kernel (one half-wave = 32 channels
+    x TP_NPH consecutive receivers, streaming their receiver-sorted in-edges; register
+    accumulators flushed at receiver boundaries), but the rows of edge e+1 -- the path group's
+    x blocks of x[sender], the SH row, the group's weight slices -- travel by
+    ``global_load_lds_dwordx4`` into a per-half-wave LDS image while edge e computes, instead of
+    into a second register set.  Each half-wave's rows are a static list of 16-B chunks; a
+    wave-instruction moves 64 chunks of ONE half-wave's list (all 64 lanes, per-lane source
+    addresses from wave-uniform row bases read with v_readlane), so the image is lane-linear
+    as LDS-DMA requires.  The loop is wave-uniform (a half-wave that has finished computes
+    discarded values), because an LDS-DMA instruction needs every lane."""
+    WPB = TP_FWD_WPB
+    TN = 2 * WPB * TP_NPH
+    ng = len(groups)
+    glist = []
+    for grp in groups:
+        need_l1 = sorted({p.l1 for p in grp})
+        need_l2 = sorted({p.l2 for p in grp})
+        chunks, fo_x, fo_w = [], {}, {}
+        for l in need_l1:
+            fo_x[l] = 4 * len(chunks)
+            chunks += [(0, 4 * node_off[l] + 16 * cc) for cc in range(8 * (2 * l + 1))]
+        fo_sh = 4 * len(chunks)
+        chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
+        for p in grp:
+            fo_w[p.slot] = 4 * len(chunks)
+            chunks += [(2, 4 * p.slot * MUL + 16 * cc) for cc in range(8)]
+        glist.append((need_l1, need_l2, chunks, fo_x, fo_sh, fo_w))
+    NJ = max(-(-len(g[2]) // 64) for g in glist)
+    L: List[str] = []
+    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_FWD_WPE})))" if TP_FWD_WPE else ""
+    L.append(f"__global__ __launch_bounds__({64 * WPB}){wpe} void tp_fwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    float inv_norm, float* __restrict__ agg) {")
+    L.append(f"  __shared__ float4 img_[{WPB}][2][{NJ * 64}];")
+    L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5, wv = threadIdx.x >> 6;")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
+    L.append("  if (nw0 >= n_nodes) return;   // uniform per wave; a half past the end gets no receivers")
+    L.append(f"  const int n0 = min(nw0 + hf * {TP_NPH}, n_nodes), n1 = min(n0 + {TP_NPH}, n_nodes);")
+    L.append("  float4* __restrict__ im0 = img_[wv][0];")
+    L.append("  float4* __restrict__ im1 = img_[wv][1];")
+    L.append("  const float* __restrict__ imf = reinterpret_cast<const float*>(hf ? im1 : im0);")
+    L.append("  switch (grp) {")
+    for gi, grp in enumerate(groups):
+        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
+        nj = -(-len(chunks) // 64)
+        L.append(f"  case {gi}: {{ // {len(chunks)} chunks of 16 B per half-wave and edge")
+        # per-lane chunk descriptors, loop-invariant: chunk 64 j + lane = (row kind, byte offset)
+        for j in range(nj):
+            runs = []            # (first chunk, end chunk, kind, first offset), offsets linear in a run
+            for c in range(64 * j, min(64 * j + 64, len(chunks))):
+                k, o = chunks[c]
+                if runs and runs[-1][2] == k and runs[-1][3] + 16 * (c - runs[-1][0]) == o and runs[-1][1] == c:
+                    runs[-1][1] = c + 1
+                else:
+                    runs.append([c, c + 1, k, o])
+            kexpr, oexpr = "1", "0"             # past the list: chunk 0 of the SH row (discarded)
+            for a, b, k, o in reversed(runs):
+                kexpr = f"(c_ < {b} ? {k} : {kexpr})"
+                oexpr = f"(c_ < {b} ? {o} + 16 * (c_ - {a}) : {oexpr})"
+            L.append(f"    int kd{j}, of{j}; {{ const int c_ = {64 * j} + lane; kd{j} = {kexpr}; of{j} = {oexpr}; }}")
+
+        def issue(ev, sv):
+            out = [f"    {{ const int e0_ = __builtin_amdgcn_readlane({ev}, 0), s0_ = __builtin_amdgcn_readlane({sv}, 0);",
+                   f"      const int e1_ = __builtin_amdgcn_readlane({ev}, 32), s1_ = __builtin_amdgcn_readlane({sv}, 32);"]
+            for h in (0, 1):
+                out.append(f"      {{ const char* xb = reinterpret_cast<const char*>(x + (size_t)s{h}_ * {din});")
+                out.append(f"        const char* shb = reinterpret_cast<const char*>(sh + (size_t)e{h}_ * {nshp});")
+                out.append(f"        const char* wb = reinterpret_cast<const char*>(w + (size_t)e{h}_ * {wn});")
+                for j in range(nj):
+                    out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
+                               f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
+                               f"(__attribute__((address_space(3))) void*)(im{h} + {64 * j}), 16, 0, 0);")
+                out.append("      }")
+            out.append("    }")
+            return out
+        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
+               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+               + [f"w{p.slot}" for p in grp])
+        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
+        L.append("    int e = rowptr[n0];")
+        L.append("    const int eend = rowptr[n1];")
+        L.append("    int node = n0, nend = rowptr[min(n0 + 1, n1)], nend2 = rowptr[min(n0 + 2, n1)];")
+        L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
+        L += issue("(e < eend ? e : 0)", "(e < eend ? sender[e] : 0)")
+        L.append("    for (;;) {")
+        L.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // edge e\'s rows are in LDS')
+        L.append("      float " + ", ".join(cur) + ";")
+        for l in need_l1:
+            d = 2 * l + 1
+            L += ["      " + ln for ln in vec_load([f"x{l}_{i}" for i in range(d)], "imf", f"{fo_x[l]} + u * {d}")]
+        L += ["      " + ln for ln in sh_load(need_l2, "", f"(imf + {fo_sh})")]
+        for p in grp:
+            L.append(f"      w{p.slot} = imf[{fo_w[p.slot]} + u];")
+        L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
+        L.append("      while (node < n1 && nend == e) {")
+        L.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            L.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                         f"{p.out_off} + u * {d3}"))
+        L.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
+        L.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
+        L.append("      }")
+        L.append("      if (!__any(e < eend)) break;")
+        L.append("      const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
+        L += ["  " + ln for ln in issue("(e + 1 < eend ? e + 1 : 0)", "s1")]
+        cpin = pin(accs + cur)
+        xn = lambda p, i: f"x{p.l1}_{i}"  # noqa: E731
+        yn = lambda p, j: f"y{p.l2 * p.l2 + j}"  # noqa: E731
+        for p in grp:
+            d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
+            fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
+            if fold[1] == "none":
+                _emit_t(p, xn, yn, "t", L, "        ")
+                for k in range(d3):
+                    L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+            else:
+                if fold[1] == "x":
+                    for i in range(d1):
+                        L.append(f"        const float xw{i} = {xn(p, i)} * wp;")
+                    xf, yf = (lambda p, i: f"xw{i}"), yn
+                else:
+                    for j in range(d2):
+                        L.append(f"        const float yw{j} = {yn(p, j)} * wp;")
+                    xf, yf = xn, (lambda p, j: f"yw{j}")
+                _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", L, "        ")
+            L.append("      }")
+            L.append("      " + cpin)
+        L.append("      s1 = s2; ++e;")
+        L.append("    }")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -306,113 +667,118 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
-    L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
-    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
-    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
-    L.append("    float inv_norm, float* __restrict__ agg) {")
-    L.append("  const int lane = threadIdx.x & 63;")
-    L.append(f"  const int u = lane & {MUL - 1};")
-    # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the x
-    # rows of a lattice are gathered by one XCD (its L2) rather than by all eight (r03h: 1828
-    # -> 1865 graphs/s together with the 64-accumulator groups)
-    TN = 2 * TP_FWD_WPB * TP_NPH          # receivers per node tile (one workgroup)
-    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
-    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
-    L.append(f"  const int n0 = ((tile * {TP_FWD_WPB} + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
-    L.append("  if (n0 >= n_nodes) return;")
-    L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
-    L.append("  switch (grp) {")
-    for gi, grp in enumerate(groups):
-        L.append(f"  case {gi}: {{")
-        need_l1 = sorted({p.l1 for p in grp})
-        need_l2 = sorted({p.l2 for p in grp})
-        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
-        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
-        cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
-               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
-               + [f"w{p.slot}" for p in grp])
+    if TP_FWD_GLDS == 2 and not bf:
+        L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off)
+    elif TP_FWD_GLDS and not bf:
+        L += _emit_tp_fwd_glds(name, groups, din, nshp, dmid, wn, node_off)
+    else:
+        L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
+        L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+        L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+        L.append("    float inv_norm, float* __restrict__ agg) {")
+        L.append("  const int lane = threadIdx.x & 63;")
+        L.append(f"  const int u = lane & {MUL - 1};")
+        # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the x
+        # rows of a lattice are gathered by one XCD (its L2) rather than by all eight (r03h: 1828
+        # -> 1865 graphs/s together with the 64-accumulator groups)
+        TN = 2 * TP_FWD_WPB * TP_NPH          # receivers per node tile (one workgroup)
+        L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
+        L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+        L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+        L.append(f"  const int n0 = ((tile * {TP_FWD_WPB} + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
+        L.append("  if (n0 >= n_nodes) return;")
+        L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
+        L.append("  switch (grp) {")
+        for gi, grp in enumerate(groups):
+            L.append(f"  case {gi}: {{")
+            need_l1 = sorted({p.l1 for p in grp})
+            need_l2 = sorted({p.l2 for p in grp})
+            accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+            L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
+            cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
+                   + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+                   + [f"w{p.slot}" for p in grp])
 
-        def load(pref, ev, sv, guard):
-            # addresses stay in bounds when the edge does not exist (index 0); the loaded
-            # values of a missing edge are never used
-            out = [f"    {{ const bool ok = {guard};",
-                   f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
-                   f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
-                   f"      const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
-            for l in need_l1:
-                d = 2 * l + 1
-                out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
-                                                          f"{node_off[l]} + u * {d}")]
-            out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
-            for p in grp:
-                out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
-            out.append("    }")
-            return out
-        L.append("    int e = rowptr[n0];")
-        L.append("    const int eend = rowptr[n1];")
-        L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
-        L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
-        L.append("    float " + ", ".join(cur) + ";")
-        L += load("", "e", "(e < eend ? sender[e] : 0)", "e < eend")
-        gpin = pin(accs + cur)
-        def step(cp, np_):
-            """one pipelined edge step: flush finished receivers, issue edge e+1's loads
-            into the ``np_`` register set, compute edge e from the ``cp`` set"""
-            out = []
-            # flush every receiver whose range ends here (also covers receivers with no in-edges)
-            out.append("      while (node < n1 && nend == e) {")
-            out.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
-            for p in grp:
-                d3 = 2 * p.l3 + 1
-                out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                             f"{p.out_off} + u * {d3}"))
-            out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
-            out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
-            out.append("      }")
-            out.append("      if (e >= eend) break;")
-            out.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
-            out.extend("  " + ln for ln in load(np_, "e + 1", "s1", "e + 1 < eend"))
-            cpin = pin(accs + [cp + v for v in cur] + [np_ + v for v in cur])
-            # the in-flight next-edge registers are pinned only after the last path, so no
-            # earlier path boundary waits for the prefetch to land
-            cpin_mid = pin(accs + [cp + v for v in cur])
-            xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
-            yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
-            for p in grp:
-                d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
-                out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-                out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
-                fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
-                if fold[1] == "none":
-                    _emit_t(p, xn, yn, "t", out, "        ")
-                    for k in range(d3):
-                        out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
-                else:
-                    # fold the path weight into the shorter of x / y (d1 or d2 products instead
-                    # of d3 + 1) and accumulate the CG terms straight into the accumulators
-                    if fold[1] == "x":
-                        for i in range(d1):
-                            out.append(f"        const float xw{i} = {xn(p, i)} * wp;")
-                        xf, yf = (lambda p, i: f"xw{i}"), yn
-                    else:
-                        for j in range(d2):
-                            out.append(f"        const float yw{j} = {yn(p, j)} * wp;")
-                        xf, yf = xn, (lambda p, j: f"yw{j}")
-                    _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", out, "        ")
+            def load(pref, ev, sv, guard):
+                # addresses stay in bounds when the edge does not exist (index 0); the loaded
+                # values of a missing edge are never used
+                out = [f"    {{ const bool ok = {guard};",
+                       f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
+                       f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
+                       f"      const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
+                for l in need_l1:
+                    d = 2 * l + 1
+                    out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
+                                                              f"{node_off[l]} + u * {d}")]
+                out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
+                for p in grp:
+                    out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
+                out.append("    }")
+                return out
+            L.append("    int e = rowptr[n0];")
+            L.append("    const int eend = rowptr[n1];")
+            L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
+            L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
+            L.append("    float " + ", ".join(cur) + ";")
+            L += load("", "e", "(e < eend ? sender[e] : 0)", "e < eend")
+            gpin = pin(accs + cur)
+            def step(cp, np_):
+                """one pipelined edge step: flush finished receivers, issue edge e+1's loads
+                into the ``np_`` register set, compute edge e from the ``cp`` set"""
+                out = []
+                # flush every receiver whose range ends here (also covers receivers with no in-edges)
+                out.append("      while (node < n1 && nend == e) {")
+                out.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
+                for p in grp:
+                    d3 = 2 * p.l3 + 1
+                    out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
+                                                                 f"{p.out_off} + u * {d3}"))
+                out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
+                out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
                 out.append("      }")
-                out.append("      " + (cpin if p is grp[-1] else cpin_mid))
-            out.append("      s1 = s2; ++e; }")
-            return out
-        L.append("    for (;;) {")
-        L.append("      float " + ", ".join("n" + v for v in cur) + ";")
-        L += step("", "n")
-        L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
-        L.append("    }")
-        L.append("    break; }")
-    L.append("  default: break;")
-    L.append("  }")
-    L.append("}")
+                out.append("      if (e >= eend) break;")
+                out.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
+                out.extend("  " + ln for ln in load(np_, "e + 1", "s1", "e + 1 < eend"))
+                cpin = pin(accs + [cp + v for v in cur] + [np_ + v for v in cur])
+                # the in-flight next-edge registers are pinned only after the last path, so no
+                # earlier path boundary waits for the prefetch to land
+                cpin_mid = pin(accs + [cp + v for v in cur])
+                xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
+                yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
+                for p in grp:
+                    d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
+                    out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+                    out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
+                    fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
+                    if fold[1] == "none":
+                        _emit_t(p, xn, yn, "t", out, "        ")
+                        for k in range(d3):
+                            out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
+                    else:
+                        # fold the path weight into the shorter of x / y (d1 or d2 products instead
+                        # of d3 + 1) and accumulate the CG terms straight into the accumulators
+                        if fold[1] == "x":
+                            for i in range(d1):
+                                out.append(f"        const float xw{i} = {xn(p, i)} * wp;")
+                            xf, yf = (lambda p, i: f"xw{i}"), yn
+                        else:
+                            for j in range(d2):
+                                out.append(f"        const float yw{j} = {yn(p, j)} * wp;")
+                            xf, yf = xn, (lambda p, j: f"yw{j}")
+                        _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", out, "        ")
+                    out.append("      }")
+                    out.append("      " + (cpin if p is grp[-1] else cpin_mid))
+                out.append("      s1 = s2; ++e; }")
+                return out
+            L.append("    for (;;) {")
+            L.append("      float " + ", ".join("n" + v for v in cur) + ";")
+            L += step("", "n")
+            L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
+            L.append("    }")
+            L.append("    break; }")
+        L.append("  default: break;")
+        L.append("  }")
+        L.append("}")
 
     # ---------------- backward (per edge) ----------------
     # grouped by input block l1: each group owns a disjoint slice of gxe, so no
@@ -1221,7 +1587,9 @@ def main(outdir: str) -> None:
              "typedef float eelg_f4u __attribute__((ext_vector_type(4), aligned(4)));",
              "typedef float eelg_f3u __attribute__((ext_vector_type(3), aligned(4)));",
              "typedef float eelg_f2u __attribute__((ext_vector_type(2), aligned(4)));",
-             "typedef float eelg_f4a __attribute__((ext_vector_type(4)));", ""]
+             "typedef float eelg_f4a __attribute__((ext_vector_type(4)));",
+             "typedef float eelg_f4r __attribute__((ext_vector_type(4)));",
+             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     tp_table, sc_table = [], []
