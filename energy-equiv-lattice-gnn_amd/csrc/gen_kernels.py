@@ -42,7 +42,7 @@ TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
 # tp_fwd: the next edge's x / SH / weight rows prefetched into LDS by LDS-DMA (global_load_lds)
 # instead of a second register set (fp32 storage only)
-TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "0"))
+TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
 # LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
 TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
