@@ -449,6 +449,11 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
+  // the fp32 kernel moves x / SH / weight rows by LDS-DMA in 16-B pieces (every row length is a
+  // multiple of 16 B, so aligned bases keep every piece aligned)
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(sh) |
+        reinterpret_cast<uintptr_t>(w)) & 15) != 0)
+    return fail(-2, "tp_fwd: x, sh and w must be 16-byte aligned");
   hipLaunchKernelGGL(c->fwd, tp_fwd_grid(*c, n_nodes), dim3(64 * c->fwpb), 0, (hipStream_t)stream, x,
                      sh, w, sender, rowptr, n_nodes, inv_norm, agg);
   return check_launch("tp_fwd");

@@ -55,7 +55,8 @@ int eelg_edge_embed(const float* pos, const int* sender, const int* receiver, co
 
 /* Fused interaction: agg[n] = inv_norm * sum_{e: recv(e)=n} TP_uvu(x[sender(e)], sh[e], w[e]).
  * Replaces conv_tp(node_feats[sender], edge_attrs, tp_weights) followed by
- * scatter(..., reduce='sum') / agg_norm_const (gnn/blocks.py:591-597). */
+ * scatter(..., reduce='sum') / agg_norm_const (gnn/blocks.py:591-597).
+ * x, sh and w must be 16-byte aligned (the rows travel by LDS-DMA in 16-B pieces); -2 otherwise. */
 int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
                 const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream);
 

@@ -350,6 +350,45 @@ def test_symcon_misaligned_rows():
                                    _lib.stream(out)), "sc_fwd")
 
 
+def test_tp_fwd_misaligned_rows():
+    """The fp32 interaction kernel moves x / SH / weight rows by LDS-DMA in 16-byte pieces: x
+    and w views at a 4-byte offset are copied by the host op (same result, bitwise, forward and
+    backward), and the C-ABI rejects a misaligned pointer."""
+    from gnn import _lib, cg, ops
+    from gnn.irreps import Irreps
+    from helpers import batch
+    b, rmax = batch(4, 50, 200, 1234)
+    bd = b.to(DEV)
+    csr = ops.EdgeCSR.build(bd.edge_index, b.node_attrs.shape[0])
+    sh_ir = Irreps.spherical_harmonics(4)
+    node = Irreps("32x0e+32x1o+32x2e+32x3o+32x4e")
+    target = (sh_ir * 32).sort()[0].simplify()
+    idx, info = _lib.tp_config_by_sig(cg.fnv1a64(cg.tp_signature(node, sh_ir, target)))
+    sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[csr.perm],
+                           bd.edge_attr[csr.perm].reshape(-1), 4, 6, 0.6, rmax)
+    torch.manual_seed(6)
+    n, e = csr.num_nodes, csr.num_edges
+    xbuf = torch.randn(n * info["din"] + 1, device=DEV)
+    wbuf = torch.randn(e * info["wn"] + 1, device=DEV)
+    xm, wm = xbuf[1:].view(n, info["din"]), wbuf[1:].view(e, info["wn"])
+    assert xm.data_ptr() % 16 != 0 and wm.data_ptr() % 16 != 0
+    g = torch.randn(n, info["dmid"], device=DEV)
+    outs = []
+    for xx, ww in ((xm, wm), (xm.clone(), wm.clone())):
+        xx, ww = xx.detach().requires_grad_(True), ww.detach().requires_grad_(True)
+        agg = ops.tp_interaction(xx, sh, ww, csr, idx, info, 0.25)
+        (agg * g).sum().backward()
+        outs.append((agg, xx.grad, ww.grad))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    lib = _lib.load()
+    out = torch.empty(n, info["dmid"], device=DEV)
+    with pytest.raises(_lib.EELGError):
+        _lib.check(lib.eelg_tp_fwd(idx, _lib.ptr(xm), _lib.ptr(sh), _lib.ptr(wm.contiguous()),
+                                   _lib.ptr(csr.sender), _lib.ptr(csr.rowptr), n, 0.25,
+                                   _lib.ptr(out), _lib.stream(out)), "tp_fwd")
+
+
 def test_stream_overlap_matches_in_line_bitwise():
     """The side-stream overlap (radial MLPs, contraction coefficients and their gradients,
     linear weight gradients) changes only where kernels run, not what they compute: the
