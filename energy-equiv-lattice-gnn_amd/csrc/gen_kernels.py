@@ -40,8 +40,10 @@ TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 # workgroups refill a freed wave slot at once: r03z kbench 0.505 vs 0.520 ms at 4, 0.518 at 2;
 # in the step 0.438 vs 0.446 ms)
 TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
-# tp_fwd: the next edge's x / SH / weight rows prefetched into LDS by LDS-DMA (global_load_lds)
-# instead of a second register set (fp32 storage only)
+# tp_fwd: the rows of the next two edges (x / SH / weight) prefetched into LDS by LDS-DMA
+# (global_load_lds) instead of a second register set (fp32 storage only); 0 = the register
+# pipeline (the bf16-storage kernel's form).  One edge in flight by LDS-DMA measured slower
+# (r03ag/r03ai: 0.499 vs 0.486 ms kbench) and was removed.
 TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
 # LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
 TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
@@ -375,6 +377,7 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]
     L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
     L.append("  if (nw0 >= n_nodes) return;   // uniform per wave; a half past the end gets no receivers")
     L.append("  float4* __restrict__ ib = &img_[wv][0][0][0];")
+    L.append("  const char* pad_ = reinterpret_cast<const char*>(eelg_tp_pad);")
     L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)ib);")
     for h in (0, 1):
         L.append(f"  const int n0_{h} = min(nw0 + {h * TP_NPH}, n_nodes), n1_{h} = min(n0_{h} + {TP_NPH}, n_nodes);")
@@ -392,11 +395,13 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]
         def issue(buf, ahead):
             out = ["    {"]
             for h in (0, 1):
-                out.append(f"      {{ const int ee_ = e_{h} + {ahead} < eend_{h} ? e_{h} + {ahead} : 0;")
-                out.append(f"        const int ss_ = e_{h} + {ahead} < eend_{h} ? sender[ee_] : 0;")
-                out.append(f"        const char* xb = reinterpret_cast<const char*>(x + (size_t)ss_ * {din});")
-                out.append(f"        const char* shb = reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp});")
-                out.append(f"        const char* wb = reinterpret_cast<const char*>(w + (size_t)ee_ * {wn});")
+                # a half past its last edge reads the pad row (no edge row need exist: E = 0)
+                out.append(f"      {{ const bool ok_ = e_{h} + {ahead} < eend_{h};")
+                out.append(f"        const int ee_ = ok_ ? e_{h} + {ahead} : 0;")
+                out.append(f"        const int ss_ = ok_ ? sender[ee_] : 0;")
+                out.append(f"        const char* xb = ok_ ? reinterpret_cast<const char*>(x + (size_t)ss_ * {din}) : pad_;")
+                out.append(f"        const char* shb = ok_ ? reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp}) : pad_;")
+                out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")
                 out.append(f"        float4* dst = ib + ({buf}) * {2 * NI} + {h * NI};")
                 for j in range(nj):
                     out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
@@ -484,154 +489,6 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]
     return L
 
 
-def _emit_tp_fwd_glds(name, groups, din, nshp, dmid, wn, node_off) -> List[str]:
-    """tp_fwd with the next edge's rows prefetched into LDS by LDS-DMA.
-
-    Same mapping and arithmetic as the register-pipelined kernel (one half-wave = 32 channels
-    x TP_NPH consecutive receivers, streaming their receiver-sorted in-edges; register
-    accumulators flushed at receiver boundaries), but the rows of edge e+1 -- the path group's
-    x blocks of x[sender], the SH row, the group's weight slices -- travel by
-    ``global_load_lds_dwordx4`` into a per-half-wave LDS image while edge e computes, instead of
-    into a second register set.  Each half-wave's rows are a static list of 16-B chunks; a
-    wave-instruction moves 64 chunks of ONE half-wave's list (all 64 lanes, per-lane source
-    addresses from wave-uniform row bases read with v_readlane), so the image is lane-linear
-    as LDS-DMA requires.  The loop is wave-uniform (a half-wave that has finished computes
-    discarded values), because an LDS-DMA instruction needs every lane."""
-    WPB = TP_FWD_WPB
-    TN = 2 * WPB * TP_NPH
-    ng = len(groups)
-    glist = []
-    for grp in groups:
-        need_l1 = sorted({p.l1 for p in grp})
-        need_l2 = sorted({p.l2 for p in grp})
-        chunks, fo_x, fo_w = [], {}, {}
-        for l in need_l1:
-            fo_x[l] = 4 * len(chunks)
-            chunks += [(0, 4 * node_off[l] + 16 * cc) for cc in range(8 * (2 * l + 1))]
-        fo_sh = 4 * len(chunks)
-        chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
-        for p in grp:
-            fo_w[p.slot] = 4 * len(chunks)
-            chunks += [(2, 4 * p.slot * MUL + 16 * cc) for cc in range(8)]
-        glist.append((need_l1, need_l2, chunks, fo_x, fo_sh, fo_w))
-    NJ = max(-(-len(g[2]) // 64) for g in glist)
-    L: List[str] = []
-    wpe = f" __attribute__((amdgpu_waves_per_eu({TP_FWD_WPE})))" if TP_FWD_WPE else ""
-    L.append(f"__global__ __launch_bounds__({64 * WPB}){wpe} void tp_fwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
-    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
-    L.append("    float inv_norm, float* __restrict__ agg) {")
-    L.append(f"  __shared__ float4 img_[{WPB}][2][{NJ * 64}];")
-    L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5, wv = threadIdx.x >> 6;")
-    L.append(f"  const int u = lane & {MUL - 1};")
-    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
-    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
-    L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
-    L.append("  if (nw0 >= n_nodes) return;   // uniform per wave; a half past the end gets no receivers")
-    L.append(f"  const int n0 = min(nw0 + hf * {TP_NPH}, n_nodes), n1 = min(n0 + {TP_NPH}, n_nodes);")
-    L.append("  float4* __restrict__ im0 = img_[wv][0];")
-    L.append("  float4* __restrict__ im1 = img_[wv][1];")
-    L.append("  const float* __restrict__ imf = reinterpret_cast<const float*>(hf ? im1 : im0);")
-    L.append("  switch (grp) {")
-    for gi, grp in enumerate(groups):
-        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
-        nj = -(-len(chunks) // 64)
-        L.append(f"  case {gi}: {{ // {len(chunks)} chunks of 16 B per half-wave and edge")
-        # per-lane chunk descriptors, loop-invariant: chunk 64 j + lane = (row kind, byte offset)
-        for j in range(nj):
-            runs = []            # (first chunk, end chunk, kind, first offset), offsets linear in a run
-            for c in range(64 * j, min(64 * j + 64, len(chunks))):
-                k, o = chunks[c]
-                if runs and runs[-1][2] == k and runs[-1][3] + 16 * (c - runs[-1][0]) == o and runs[-1][1] == c:
-                    runs[-1][1] = c + 1
-                else:
-                    runs.append([c, c + 1, k, o])
-            kexpr, oexpr = "1", "0"             # past the list: chunk 0 of the SH row (discarded)
-            for a, b, k, o in reversed(runs):
-                kexpr = f"(c_ < {b} ? {k} : {kexpr})"
-                oexpr = f"(c_ < {b} ? {o} + 16 * (c_ - {a}) : {oexpr})"
-            L.append(f"    int kd{j}, of{j}; {{ const int c_ = {64 * j} + lane; kd{j} = {kexpr}; of{j} = {oexpr}; }}")
-
-        def issue(ev, sv):
-            out = [f"    {{ const int e0_ = __builtin_amdgcn_readlane({ev}, 0), s0_ = __builtin_amdgcn_readlane({sv}, 0);",
-                   f"      const int e1_ = __builtin_amdgcn_readlane({ev}, 32), s1_ = __builtin_amdgcn_readlane({sv}, 32);"]
-            for h in (0, 1):
-                out.append(f"      {{ const char* xb = reinterpret_cast<const char*>(x + (size_t)s{h}_ * {din});")
-                out.append(f"        const char* shb = reinterpret_cast<const char*>(sh + (size_t)e{h}_ * {nshp});")
-                out.append(f"        const char* wb = reinterpret_cast<const char*>(w + (size_t)e{h}_ * {wn});")
-                for j in range(nj):
-                    out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
-                               f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
-                               f"(__attribute__((address_space(3))) void*)(im{h} + {64 * j}), 16, 0, 0);")
-                out.append("      }")
-            out.append("    }")
-            return out
-        accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
-        cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
-               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
-               + [f"w{p.slot}" for p in grp])
-        L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
-        L.append("    int e = rowptr[n0];")
-        L.append("    const int eend = rowptr[n1];")
-        L.append("    int node = n0, nend = rowptr[min(n0 + 1, n1)], nend2 = rowptr[min(n0 + 2, n1)];")
-        L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
-        L += issue("(e < eend ? e : 0)", "(e < eend ? sender[e] : 0)")
-        L.append("    for (;;) {")
-        L.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // edge e\'s rows are in LDS')
-        L.append("      float " + ", ".join(cur) + ";")
-        for l in need_l1:
-            d = 2 * l + 1
-            L += ["      " + ln for ln in vec_load([f"x{l}_{i}" for i in range(d)], "imf", f"{fo_x[l]} + u * {d}")]
-        L += ["      " + ln for ln in sh_load(need_l2, "", f"(imf + {fo_sh})")]
-        for p in grp:
-            L.append(f"      w{p.slot} = imf[{fo_w[p.slot]} + u];")
-        L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
-        L.append("      while (node < n1 && nend == e) {")
-        L.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
-        for p in grp:
-            d3 = 2 * p.l3 + 1
-            L.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                         f"{p.out_off} + u * {d3}"))
-        L.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
-        L.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
-        L.append("      }")
-        L.append("      if (!__any(e < eend)) break;")
-        L.append("      const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
-        L += ["  " + ln for ln in issue("(e + 1 < eend ? e + 1 : 0)", "s1")]
-        cpin = pin(accs + cur)
-        xn = lambda p, i: f"x{p.l1}_{i}"  # noqa: E731
-        yn = lambda p, j: f"y{p.l2 * p.l2 + j}"  # noqa: E731
-        for p in grp:
-            d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
-            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-            L.append(f"        const float wp = w{p.slot} * ({flit(p.coef)} * inv_norm);")
-            fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
-            if fold[1] == "none":
-                _emit_t(p, xn, yn, "t", L, "        ")
-                for k in range(d3):
-                    L.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
-            else:
-                if fold[1] == "x":
-                    for i in range(d1):
-                        L.append(f"        const float xw{i} = {xn(p, i)} * wp;")
-                    xf, yf = (lambda p, i: f"xw{i}"), yn
-                else:
-                    for j in range(d2):
-                        L.append(f"        const float yw{j} = {yn(p, j)} * wp;")
-                    xf, yf = xn, (lambda p, j: f"yw{j}")
-                _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", L, "        ")
-            L.append("      }")
-            L.append("      " + cpin)
-        L.append("      s1 = s2; ++e;")
-        L.append("    }")
-        L.append("    break; }")
-    L.append("  default: break;")
-    L.append("  }")
-    L.append("}")
-    return L
-
-
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -669,8 +526,6 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     ng = len(groups)
     if TP_FWD_GLDS == 2 and not bf:
         L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off)
-    elif TP_FWD_GLDS and not bf:
-        L += _emit_tp_fwd_glds(name, groups, din, nshp, dmid, wn, node_off)
     else:
         L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
         L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
@@ -700,12 +555,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
                    + [f"w{p.slot}" for p in grp])
 
             def load(pref, ev, sv, guard):
-                # addresses stay in bounds when the edge does not exist (index 0); the loaded
-                # values of a missing edge are never used
+                # a missing edge reads the pad row (x row 0 exists since N > 0, but no edge row
+                # need exist: E = 0); the loaded values of a missing edge are never used
                 out = [f"    {{ const bool ok = {guard};",
                        f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
-                       f"      const float* __restrict__ ye = sh + (size_t)(ok ? {ev} : 0) * {nshp};",
-                       f"      const {WT}* __restrict__ we = w + (size_t)(ok ? {ev} : 0) * {wn} + u;"]
+                       f"      const float* __restrict__ ye = ok ? sh + (size_t){ev} * {nshp} : eelg_tp_pad;",
+                       f"      const {WT}* __restrict__ we = (ok ? w + (size_t){ev} * {wn} : "
+                       f"reinterpret_cast<const {WT}*>(eelg_tp_pad)) + u;"]
                 for l in need_l1:
                     d = 2 * l + 1
                     out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
@@ -1592,6 +1448,11 @@ def main(outdir: str) -> None:
              "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
+    # the row a tp_fwd stream reads for an edge past its range (also when the batch has no
+    # edges and the edge tensors are empty): as long as the longest x / SH / weight row
+    pad = max(max(node.dim, (sh.dim + 3) // 4 * 4, sum(p.mul for p in cg.tp_paths(node, sh, target)))
+              for node, sh, target in tp_configs().values())
+    parts.append(f"__device__ __attribute__((aligned(16))) float eelg_tp_pad[{(pad + 3) // 4 * 4}];\n")
     tp_table, sc_table = [], []
     for name, (node, sh, target) in tp_configs().items():
         code, info = emit_tp(name, node, sh, target)

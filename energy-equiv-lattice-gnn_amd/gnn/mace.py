@@ -137,15 +137,18 @@ class SymmetricContraction(torch.nn.Module):
         reference computes with that U and the loaded weights.  A U with symmetric weight on
         monomials the generated kernels do not evaluate raises.
 
-        Every load starts from the derived basis: a block not carried by (or equal to the
-        derived one in) this checkpoint goes back to the derived block, so loading a standard
-        checkpoint after one in another basis computes with the derived U again.  The adopted
+        Every load that carries U buffers for this module starts from the derived basis: a
+        block not carried by (or equal to the derived one in) this checkpoint goes back to the
+        derived block, so loading a standard checkpoint after one in another basis computes
+        with the derived U again.  A load with no U buffer of this module (a weights-only
+        partial load) keeps the basis in use.  The adopted
         blocks are computed first and written only when every U of the module checked out."""
         plan = None
-        adopted, loaded, failed = [], {}, False
+        adopted, loaded, failed, seen = [], {}, False, False
         for l, nu, key in list(self._u_keys(prefix)):
             if key not in state_dict:
                 continue
+            seen = True
             u = state_dict.pop(key).detach().to("cpu", torch.float64)
             want = cg.reference_U_shape(self._coupling, l, nu)
             if tuple(u.shape) != want:
@@ -165,7 +168,7 @@ class SymmetricContraction(torch.nn.Module):
                 continue
             adopted.append((k0, block))
             loaded[(l, nu)] = u.to(torch.float32)
-        if not failed:
+        if seen and not failed:
             plan = plan or cg.symcon_plan(self._coupling, self._ls, self.correlation)
             fresh = torch.tensor(plan.ubig, dtype=torch.float64)
             for k0, block in adopted:

@@ -30,8 +30,8 @@ class FlatGradAllReduce:
     Packing is one ``torch.cat`` and unpacking one ``_foreach_copy_`` (a handful of
     launches instead of two copies per parameter), so the exchange costs one RCCL
     all-reduce plus O(1) kernels per step.  A parameter without a gradient on this rank
-    contributes zeros (one cached zero tensor, no per-step fill) and receives the averaged
-    slice as a view of the reduced buffer."""
+    contributes zeros (one cached zero tensor, no per-step fill) and receives a copy of the
+    averaged slice."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], group=None):
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
@@ -64,7 +64,8 @@ class FlatGradAllReduce:
             torch._foreach_copy_([g for g, _ in have], [v for _, v in have])
         for p, v in zip(self.params, views):
             if p.grad is None:
-                p.grad = v.view_as(p)
+                # a copy, not a view: a view would keep the whole flat buffer alive
+                p.grad = v.view_as(p).clone()
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:

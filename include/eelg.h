@@ -153,7 +153,11 @@ int eelg_segment_order(const float* src, const int* rowptr, int n_rows, int widt
 /* Backward: grad_src for every row of every segment (rows outside all segments are not
  * written): max / min -> grad_out at arg, 0 elsewhere (the whole gradient to one element, as
  * torch_scatter's scatter_max / scatter_min); mul -> grad_out times the product of the
- * segment's other entries (prefix x suffix products, exact at zeros). */
+ * segment's other entries (prefix x suffix products, exact at zeros).
+ * Deliberate differences from torch_scatter on CUDA (parity unpinned, the oracle's torch.prod /
+ * torch.max agree with these kernels): scatter_mul's backward divides the product by src, so
+ * an entry that is exactly 0 gives NaN/inf there and a finite gradient here; scatter_max /
+ * scatter_min on CUDA pick the arg of a tie by an atomic race, here it is always the first. */
 int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, const float* grad_out,
                            int n_rows, int width, int op, float* grad_src, void* stream);
 

@@ -204,3 +204,21 @@ def test_reference_U_shapes():
     assert cg.reference_U_shape("0e+1o+2e+3o+4e", 0, 3) == (25, 25, 25, 42)
     assert cg.reference_U_shape("0e+1o+2e+3o+4e", 4, 3) == (9, 25, 25, 25, 150)
     assert cg.reference_U_shape("0e+1o+2e+3o+4e", 0, 1) == (25, 1)
+
+
+def test_weights_only_partial_load_keeps_an_adopted_basis():
+    """a ``strict=False`` load carrying no U buffers (weights only) must not reset
+    an adopted U basis: the coefficients, hence the outputs, stay the same."""
+    o, m = _pair(2, 4)
+    sd = o.state_dict()
+    sc_key = "stiffness_head.layers.1.product.symmetric_contractions"
+    _rotate_U_basis(sd, f"{sc_key}.contractions.32x2e", 3, 1)
+    m.load_state_dict(sd, strict=True)
+    sc = m.stiffness_head.layers[1].product.symmetric_contractions
+    u_adopted = sc.u_sym.clone()
+    coef = sc.coefficients().detach().clone()
+    weights_only = {k: v for k, v in sd.items() if "U_matrix" not in k}
+    m.load_state_dict(weights_only, strict=False)
+    assert len(sc._u_loaded) == 1
+    assert torch.equal(sc.u_sym, u_adopted)
+    assert torch.equal(sc.coefficients().detach(), coef)

@@ -143,3 +143,48 @@ def test_edge_cases_vs_oracle():
     assert err < 1e-4, err
     assert gerr < 2e-5, gerr
     assert err1 < 1e-4 and gerr1 < 2e-5
+
+
+def test_edgeless_batch_vs_oracle():
+    """A batch made only of edgeless graphs (E = 0, N > 0): the interaction aggregates are
+    zeros (torch_scatter's ``scatter(..., dim_size=N)`` of no messages,
+    ``/root/reference/gnn/blocks.py:595-597``), and the model, fwd + bwd, matches the oracle.
+    The edge tensors are empty (null data pointers): no kernel may read an edge row."""
+    from gnn.data import collate
+    b = collate([_graph(5, [], seed=1), _graph(9, [], seed=4), _graph(33, [], seed=8)])
+    assert b.edge_index.shape[1] == 0
+    err, gerr = _oracle_pair(b, 0.05)
+    record_parity("edgeless_batch", stiffness=err, grad_params=gerr)
+    assert err < 1e-4, err
+    assert gerr < 1e-5, gerr
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_tp_fwd_with_no_edges_writes_zeros(bf16):
+    """``eelg_tp_fwd`` / ``eelg_tp_fwd_bf16`` directly with E = 0 and N = 70 (several node
+    tiles and both half-waves): every aggregate row is written, and it is zero."""
+    from gnn import _lib, cg, ops
+    from gnn.irreps import Irreps
+    n = 70
+    sh_ir = Irreps.spherical_harmonics(4)
+    node = Irreps("32x0e+32x1o+32x2e+32x3o+32x4e")
+    target = (sh_ir * 32).sort()[0].simplify()
+    idx, info = _lib.tp_config_by_sig(cg.fnv1a64(cg.tp_signature(node, sh_ir, target)))
+    csr = ops.EdgeCSR.build(torch.zeros(2, 0, dtype=torch.long, device=DEV), n)
+    assert int(csr.rowptr[-1]) == 0
+    x = torch.randn(n, info["din"], device=DEV)
+    sh = torch.empty(0, 28, device=DEV)
+    w = torch.empty(0, info["wn"], device=DEV, dtype=torch.bfloat16 if bf16 else torch.float32)
+    out = torch.full((n, info["dmid"]), float("nan"), device=DEV)
+    lib = _lib.load()
+    fn = lib.eelg_tp_fwd_bf16 if bf16 else lib.eelg_tp_fwd
+    _lib.check(fn(idx, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
+                  _lib.ptr(csr.rowptr), n, 0.25, _lib.ptr(out), _lib.stream(out)), "tp_fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.zeros_like(out))
+    # and through the autograd op, backward included (grad_x of no messages is zero)
+    xx = x.clone().requires_grad_(True)
+    agg = ops.tp_interaction(xx, sh[:, :25], w, csr, idx, info, 0.25)
+    agg.sum().backward()
+    assert torch.equal(agg, torch.zeros_like(agg))
+    assert torch.equal(xx.grad, torch.zeros_like(xx.grad))
