@@ -116,17 +116,25 @@ def tp_fwd_bytes(n: int, e: int, din: int, w: int, dmid: int, nsh: int = 25, wby
     return 4 * (n * din + e * nsh + e + (n + 1) + n * dmid) + wbytes * e * w
 
 
+def workload_key(args) -> str:
+    """Key of this command's workload in profiles/pmc_traffic.json (tools/summarize_profile.py)."""
+    if args.model != "egnn":
+        return f"{args.model}_b{args.batch}_n{args.nodes}_e{args.edges}"
+    return (f"egnn_b{args.batch}_n{args.nodes}_e{args.edges}_L{args.layers}_lmax{args.lmax}_"
+            f"{args.storage}")
+
+
 def pmc_traffic(kernel: str, args) -> dict | None:
     """HBM bytes per launch of ``kernel`` from the committed PMC table (profiles/pmc_traffic.json,
     written by tools/summarize_profile.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes
-    of this same default command).  Only valid for the default workload; None otherwise."""
-    if (args.batch, args.nodes, args.edges, args.layers, args.lmax, args.storage) != \
-            (32, 1024, 4096, 4, 4, "float32"):
-        return None
+    of this same command: tools/profile_round.sh with BENCH_ARGS), looked up under this
+    command's workload key; None when that workload has no committed passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
-    tab = json.load(open(path))
+    tab = json.load(open(path)).get("workloads", {}).get(workload_key(args))
+    if tab is None:
+        return None
     hits = [v for k, v in tab["kernels"].items() if k.split("|")[0] == kernel]
     if not hits:
         return None
@@ -138,7 +146,7 @@ def pmc_traffic(kernel: str, args) -> dict | None:
     fetch = FETCH_CORRECTION * fetch_raw
     return {"bytes": round(fetch + write), "fetch": round(fetch), "write": round(write),
             "fetch_raw": round(fetch_raw), "fetch_correction": FETCH_CORRECTION,
-            "source": f"profiles/pmc_traffic.json ({tab['source']}), "
+            "source": f"profiles/pmc_traffic.json [{workload_key(args)}] ({tab['source']}), "
                       "calibration profiles/r02_fetch_calibration.md"}
 
 
@@ -314,8 +322,12 @@ def main_cgc(args):
             ach = byts / (ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "traffic_detail": pmc_traffic("cgc_fwd_kernel", args),
                     "kernel": "cgc_fwd (fused gather + softplus*sigmoid + segmented sum)",
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum["cgc_fwd"]["count"]}
+            if roof["traffic_detail"]:
+                roof["traffic"] = roof["traffic_detail"]["bytes"]
+                roof["traffic_detail"]["ratio_to_algorithmic"] = round(roof["traffic"] / byts, 3)
         out = {"metric": f"lattice-graphs/s (fwd+bwd), {args.model} 3-layer, ~1k nodes/~4k edges",
                "value": round(world * args.batch * args.steps / dt, 2), "unit": "lattice-graphs/s",
                "n_gpus": n_dev, "ranks": world, "steps": args.steps, "warmup": args.warmup,

@@ -408,7 +408,7 @@ int eelg_sc_info(int cfg, int* info, uint64_t* sig) {
   if (cfg < 0 || cfg >= n) return fail(-1, "bad sc config %d", cfg);
   const eelg_sc_cfg& c = t[cfg];
   info[0] = c.D; info[1] = c.drow; info[2] = c.orow; info[3] = c.nterms; info[4] = c.njg;
-  info[5] = c.Dout; info[6] = c.nbc;
+  info[5] = c.Dout; info[6] = c.nbc; info[7] = c.cld;
   *sig = c.sig;
   return 0;
 }
@@ -656,7 +656,7 @@ int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  if (!a16(x) || !a16(out)) return fail(-2, "sc_fwd: x and out must be 16-byte aligned");
+  if (!a16(x) || !a16(out) || !a16(coef)) return fail(-2, "sc_fwd: x, coef and out must be 16-byte aligned");
   hipLaunchKernelGGL(c->fwd, sc_tile_grid(n_nodes, mul, c->nb), dim3(c->nth), 0,
                      (hipStream_t)stream, x, coef, n_nodes, out);
   return check_launch("sc_fwd");
@@ -672,8 +672,8 @@ int eelg_sc_bwd_x_cm(int cfg, const float* x, const float* coef, const float* gr
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  if (!a16(x) || !a16(grad_out) || !a16(grad_x))
-    return fail(-2, "sc_bwd_x: x, grad_out and grad_x must be 16-byte aligned");
+  if (!a16(x) || !a16(grad_out) || !a16(grad_x) || !a16(coef))
+    return fail(-2, "sc_bwd_x: x, coef, grad_out and grad_x must be 16-byte aligned");
   hipLaunchKernelGGL(c->bwd_x, sc_tile_grid(n_nodes, mul, c->nb), dim3(c->nth), 0,
                      (hipStream_t)stream, x, coef, grad_out, n_nodes, grad_x, xt, gt);
   return check_launch("sc_bwd_x");
@@ -756,6 +756,78 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
   hipLaunchKernelGGL(lin_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, x_row, w, bias,
                      n_nodes, y, y_row, *desc, res);
   return check_launch("linear_fwd");
+}
+
+static int lin_desc_check(const eelg_lin_desc* desc, const char* what) {
+  if (!desc || desc->n_slots <= 0 || desc->n_slots > EELG_LIN_MAXSLOT)
+    return fail(-2, "%s: bad descriptor", what);
+  for (int s = 0; s < desc->n_slots; ++s) {
+    const eelg_lin_slot& sl = desc->slot[s];
+    if (sl.n_src < 0 || sl.n_src > EELG_LIN_MAXSRC || sl.d <= 0 || sl.n_out <= 0)
+      return fail(-2, "%s: bad slot %d", what, s);
+    for (int t = 0; t < sl.n_src; ++t)
+      if (sl.src[t].k <= 0) return fail(-2, "%s: empty K in slot %d", what, s);
+  }
+  return 0;
+}
+
+static int lin_pack_check(const eelg_lin_desc* desc, const char* what) {
+  if (int rc = lin_desc_check(desc, what)) return rc;
+  for (int s = 0; s < desc->n_slots; ++s) {
+    int ks = 0;
+    for (int t = 0; t < desc->slot[s].n_src; ++t) {
+      if (desc->slot[s].src[t].k % 32) return fail(-2, "%s: source K must be a multiple of 32", what);
+      ks += desc->slot[s].src[t].k;
+    }
+    if (ks > LINX_KMAX) return fail(-2, "%s: slot %d sums K = %d > %d", what, s, ks, LINX_KMAX);
+  }
+  return 0;
+}
+
+// bf16 elements of one part of the packed weights (pack holds 3 parts = 3x this)
+long long eelg_linear_pack_size(const eelg_lin_desc* desc) {
+  if (int rc = lin_pack_check(desc, "linear_pack_size")) return rc;
+  return (long long)lin_pack_slot_off(*desc, desc->n_slots) * 8 / 3;
+}
+
+int eelg_linear_pack(const float* w, const eelg_lin_desc* desc, void* pack, void* stream) {
+  if (int rc = lin_pack_check(desc, "linear_pack")) return rc;
+  if (reinterpret_cast<uintptr_t>(pack) & 15) return fail(-2, "linear_pack: pack must be 16-byte aligned");
+  const int nunits = lin_pack_slot_off(*desc, desc->n_slots) / 3;
+  if (nunits <= 0) return 0;
+  hipLaunchKernelGGL(lin_pack_kernel, dim3((nunits + 255) / 256), dim3(256), 0, (hipStream_t)stream, w,
+                     *desc, nunits, static_cast<uint4*>(pack));
+  return check_launch("linear_pack");
+}
+
+int eelg_linear_fwd_pk(const float* x, int x_row, const void* pack, const float* bias,
+                       const float* res, int n_nodes, float* y, int y_row,
+                       const eelg_lin_desc* desc, void* stream) {
+  if (int rc = lin_pack_check(desc, "linear_fwd_pk")) return rc;
+  if (!lin_fwd_fast_ok(x, x_row, y, y_row, desc) || (reinterpret_cast<uintptr_t>(res) & 15) ||
+      (reinterpret_cast<uintptr_t>(pack) & 15))
+    return fail(-2, "linear_fwd_pk: the descriptor / rows do not qualify for the packed path "
+                    "(whole 32-wide K chunks and column tiles, d odd <= 9, 16-B aligned rows)");
+  for (int s = 0; s < desc->n_slots; ++s)
+    if (desc->slot[s].bias_off >= 0 && desc->slot[s].d != 1)
+      return fail(-2, "linear_fwd_pk: bias on a non-scalar slot");
+  if (n_nodes <= 0) return 0;
+  int max_groups = 0;
+  for (int s = 0; s < desc->n_slots; ++s) {
+    const int nb = 32 / desc->slot[s].d;
+    const int g = (n_nodes + nb - 1) / nb;
+    max_groups = g > max_groups ? g : max_groups;
+  }
+  const int gblocks = (max_groups + LINX_WAVES * LINX_GPW - 1) / (LINX_WAVES * LINX_GPW);
+  dim3 grid(((gblocks + 7) / 8) * 8 * desc->max_jt, desc->n_slots, 1);
+  const uint4* pk = static_cast<const uint4*>(pack);
+  if (res)
+    hipLaunchKernelGGL(lin_fwd_x6_kernel<true>, grid, dim3(64 * LINX_WAVES), 0, (hipStream_t)stream,
+                       x, x_row, pk, bias, n_nodes, y, y_row, *desc, res);
+  else
+    hipLaunchKernelGGL(lin_fwd_x6_kernel<false>, grid, dim3(64 * LINX_WAVES), 0, (hipStream_t)stream,
+                       x, x_row, pk, bias, n_nodes, y, y_row, *desc, res);
+  return check_launch("linear_fwd_pk");
 }
 
 int eelg_linear_fwd(const float* x, int x_row, const float* w, const float* bias, int n_nodes,

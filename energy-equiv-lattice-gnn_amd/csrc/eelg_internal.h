@@ -53,6 +53,7 @@ struct eelg_sc_cfg {
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
   int nb;                        // nodes per fwd / grad-x workgroup
   int nth;                       // threads per fwd / grad-x workgroup
+  int cld;                       // coefficient row stride (nterms rounded up to whole DMA chunks)
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);
@@ -68,6 +69,52 @@ __device__ __forceinline__ unsigned short eelg_f2bf(float f) {
   return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
 const eelg_sc_cfg* eelg_sc_table(int* n);
+
+// fp32-accurate GEMM operands on bf16 MFMA ("x6"): an fp32 value splits EXACTLY into three bf16
+// parts by truncation, x = p0 + p1 + p2 (p0 = the top 8 significant bits, p1 the next 8 of the
+// remainder, p2 the rest, which has at most 8 significant bits).  A product sum_k a_k b_k is
+// then sum over (i, j) of a_i b_j; the six part products with i + j <= 2 are computed exactly
+// by v_mfma_f32_32x32x16_bf16 and accumulated in fp32, smallest first; the three dropped ones
+// are below 2^-23 of |a_k b_k| (the error against fp64 is that of an fp32 fmaf
+// chain).  Over one K = 16 block the six 32x32x16 bf16 MFMAs (32 cycles each) take 192 cycles
+// against 512 for the eight 32x32x2 f32 MFMAs (64 cycles each): 3/8 of the f32 MFMA time.
+typedef __bf16 eelg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float eelg_f32x16v __attribute__((ext_vector_type(16)));
+
+// 8 fp32 -> three packed bf16x8 fragments (element t of the fragment = v[t])
+__device__ __forceinline__ void eelg_split8(const float* v, uint4* p) {
+  unsigned h0[8], h1[8], h2[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const unsigned a = __float_as_uint(v[t]) & 0xffff0000u;
+    const float r = v[t] - __uint_as_float(a);
+    const unsigned b = __float_as_uint(r) & 0xffff0000u;
+    h0[t] = a;
+    h1[t] = b;
+    h2[t] = __float_as_uint(r - __uint_as_float(b));
+  }
+#define EELG_PK(h, t) __builtin_amdgcn_perm(h[t + 1], h[t], 0x07060302u)
+  p[0] = make_uint4(EELG_PK(h0, 0), EELG_PK(h0, 2), EELG_PK(h0, 4), EELG_PK(h0, 6));
+  p[1] = make_uint4(EELG_PK(h1, 0), EELG_PK(h1, 2), EELG_PK(h1, 4), EELG_PK(h1, 6));
+  p[2] = make_uint4(EELG_PK(h2, 0), EELG_PK(h2, 2), EELG_PK(h2, 4), EELG_PK(h2, 6));
+#undef EELG_PK
+}
+#define EELG_MFMA_BF(acc, a, b) \
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(eelg_bf16x8, (a)), \
+                                                __builtin_bit_cast(eelg_bf16x8, (b)), acc, 0, 0, 0)
+// acc += A B over one K = 16 block, both operands split (a[3], b[3]); smallest products first
+#define EELG_X6(acc, a, b)                                                        \
+  do {                                                                          \
+    EELG_MFMA_BF(acc, (a)[0], (b)[2]); EELG_MFMA_BF(acc, (a)[1], (b)[1]);       \
+    EELG_MFMA_BF(acc, (a)[2], (b)[0]); EELG_MFMA_BF(acc, (a)[0], (b)[1]);       \
+    EELG_MFMA_BF(acc, (a)[1], (b)[0]); EELG_MFMA_BF(acc, (a)[0], (b)[0]);       \
+  } while (0)
+// acc += A B with A exactly bf16 (a single part, e.g. bf16 storage) and B split (b[3])
+#define EELG_X3(acc, a, b)                                                        \
+  do {                                                                          \
+    EELG_MFMA_BF(acc, (a), (b)[2]); EELG_MFMA_BF(acc, (a), (b)[1]);             \
+    EELG_MFMA_BF(acc, (a), (b)[0]);                                             \
+  } while (0)
 
 // Lane reduction of 64 per-lane slots: afterwards lane L holds, in v[0], the sum over all 64
 // lanes of slot L.  Recursive halving over the lane bits 32, 16, 8, 4, 2, 1: at the step on

@@ -752,3 +752,230 @@ static bool lin_fwd_fast_ok(const float* x, int x_row, const float* y, int y_row
   }
   return true;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Forward / grad-x on bf16 MFMA with fp32-accurate split operands ("x6", eelg_internal.h).
+// Same eligibility as the fp32 fast path.  The weights come pre-split, alpha-scaled and in MFMA
+// fragment order from eelg_linear_pack: for slot s, column tile jt, K chunk c (32 of the slot's
+// summed source K), K block kb and part p, 64 uint4 pieces, piece l = (hf, j) holding
+// B[k = 32c + 16kb + 8hf + t][jt*32 + j], t = 0..7.  A workgroup (LINX_WAVES = 16 waves, 4 per
+// SIMD) copies its (slot, jt) block -- 6 KB per K chunk, <= 60 KB -- into LDS once; each wave
+// stages the K chunks of its node groups through its LDS region in the natural layout exactly as
+// the fp32 path does (one chunk in flight), reads 8 consecutive k of its row per K block, splits
+// them, and runs 2 x 6 bf16 MFMAs per chunk (3/8 of the f32 MFMA time) against B fragments read
+// from LDS (ds_read_b128, conflict-free).
+// ---------------------------------------------------------------------------------------------
+#ifndef LINX_WAVES
+#define LINX_WAVES 16
+#endif
+#ifndef LINX_GPW
+#define LINX_GPW 2
+#endif
+#define LINX_KMAX 320   // summed source K of a slot held in LDS (10 chunks x 6 KB)
+
+template <int D, bool RES>
+__device__ __forceinline__ void lin_fwd_x6(const float* __restrict__ x, int x_row,
+                                           const float* __restrict__ bias, int n_nodes,
+                                           float* __restrict__ y, int y_row,
+                                           const eelg_lin_slot& sl, int g_base, int g_lim, int jt,
+                                           const uint4* __restrict__ bs, float* __restrict__ xw,
+                                           const float* __restrict__ res) {
+  using G = LinfGeom<D>;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
+  int nch = 0;
+  for (int s = 0; s < sl.n_src; ++s) nch += sl.src[s].k / 32;
+  const int my_groups = g_base + wave < g_lim ? (g_lim - g_base - wave + LINX_WAVES - 1) / LINX_WAVES : 0;
+  const int nq = my_groups * nch;
+  if (nq == 0) return;
+  const bool row_ok = i < G::NB * D;
+  const int abase = (i / D) * G::SX + (i % D) + 8 * hf * D;
+  const float bj = (sl.bias_off >= 0 && D == 1) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
+  auto chunk_of = [&](int q, int& group, int& xoff, int& c) {
+    const int k = q / nch;
+    c = q - k * nch;
+    group = g_base + k * LINX_WAVES + wave;
+    int s = 0, cc = c;
+    while (cc >= sl.src[s].k / 32) { cc -= sl.src[s].k / 32; ++s; }
+    xoff = sl.src[s].x_off + cc * 32 * D;
+  };
+  auto load = [&](int q, float4* r) {
+    int group, xoff, c;
+    chunk_of(q, group, xoff, c);
+    const int n0 = group * G::NB;
+#pragma unroll
+    for (int qq = 0; qq < G::NQ; ++qq) {
+      const int f = lane + 64 * qq;
+      const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+      const bool ok = f < G::NB * G::RUN4 && n0 + a < n_nodes;
+      r[qq] = ok ? *reinterpret_cast<const float4*>(x + (size_t)(n0 + a) * x_row + xoff + 4 * w4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  eelg_f32x16v acc;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = bj;
+  float4 ra[G::NQ];
+  load(0, ra);
+  for (int q = 0; q < nq; ++q) {
+    int group, xoff, c;
+    chunk_of(q, group, xoff, c);
+#pragma unroll
+    for (int qq = 0; qq < G::NQ; ++qq) {
+      const int f = lane + 64 * qq;
+      if (f < G::NB * G::RUN4) {
+        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+        *reinterpret_cast<float4*>(xw + a * G::SX + 4 * w4) = ra[qq];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (q + 1 < nq) load(q + 1, ra);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float av[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) av[t] = row_ok ? xw[abase + (16 * kb + t) * D] : 0.0f;
+      uint4 ap[3], bp[3];
+      eelg_split8(av, ap);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bp[p] = bs[((c * 2 + kb) * 3 + p) * 64 + lane];
+      EELG_X6(acc, ap, bp);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if ((q + 1) % nch == 0) {
+      // epilogue of the group: acc[t] = (row (t&3) + 8(t>>2) + 4hf, column i) through the wave's
+      // LDS region in the output's natural layout, then out as float4 runs
+      const int n0 = group * G::NB;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int row = (t & 3) + 8 * (t >> 2) + 4 * hf;
+        const int n = row / D, m = row - (row / D) * D;
+        if (row < G::NB * D) xw[n * G::SX + i * D + m] = acc[t];
+        acc[t] = bj;
+      }
+      __builtin_amdgcn_wave_barrier();
+      float* __restrict__ yb = y + sl.y_off + (size_t)jt * 32 * D;
+      float4 rr[G::NQ];
+      if (RES) {
+        const float* __restrict__ rb = res + sl.y_off + (size_t)jt * 32 * D;
+#pragma unroll
+        for (int qq = 0; qq < G::NQ; ++qq) {
+          const int f = min(lane + 64 * qq, G::NB * G::RUN4 - 1);
+          const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+          rr[qq] = *reinterpret_cast<const float4*>(rb + (size_t)min(n0 + a, n_nodes - 1) * y_row + 4 * w4);
+        }
+      }
+#pragma unroll
+      for (int qq = 0; qq < G::NQ; ++qq) {
+        const int f = lane + 64 * qq;
+        const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+        if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
+          const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
+          float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
+          if (RES) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
+          *reinterpret_cast<float4*>(yb + o) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// packed fragment offset (uint4 pieces) of slot s: sum over earlier slots of n_out * K / 8 ... as
+// n_jt * nch * (2 x 3 x 64) pieces per slot
+__device__ __host__ inline int lin_pack_slot_off(const eelg_lin_desc& desc, int s) {
+  int off = 0;
+  for (int t = 0; t < s; ++t) {
+    int ks = 0;
+    for (int u = 0; u < desc.slot[t].n_src; ++u) ks += desc.slot[t].src[u].k;
+    off += ((desc.slot[t].n_out + 31) / 32) * (ks / 32) * 384;
+  }
+  return off;
+}
+
+template <bool RES>
+__global__ __launch_bounds__(64 * LINX_WAVES) void lin_fwd_x6_kernel(
+    const float* __restrict__ x, int x_row, const uint4* __restrict__ pk,
+    const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
+    eelg_lin_desc desc, const float* __restrict__ res) {
+  __shared__ uint4 bs[LINX_KMAX / 32 * 384];            // this (slot, jt)'s B fragments, 60 KB
+  __shared__ float4 xw4[LINX_WAVES * LINF_XW / 4];
+  const int sidx = desc.n_slots - 1 - blockIdx.y;   // highest l (most rows) first
+  const eelg_lin_slot& sl = desc.slot[sidx];
+  // block id -> (group block gb, column tile jt): the max_jt column-tile blocks of one group
+  // block run back to back on one XCD (id % 8), so the rows they all read come from HBM once
+  const int id = blockIdx.x, xcd = id & 7, rest = id >> 3;
+  const int jt = rest % desc.max_jt, gb = (rest / desc.max_jt) * 8 + xcd;
+  const int d = sl.d;
+  if (jt * 32 >= sl.n_out) return;
+  const int nb = 32 / d;
+  const int n_groups = (n_nodes + nb - 1) / nb;
+  if (gb * LINX_WAVES * LINX_GPW >= n_groups) return;   // uniform per workgroup
+  int nch = 0;
+  for (int s = 0; s < sl.n_src; ++s) nch += sl.src[s].k / 32;
+  {
+    // the (slot, jt) block of B fragments: one contiguous run of nch x 384 pieces, all of a
+    // thread's loads issued before its LDS stores
+    const uint4* __restrict__ src = pk + lin_pack_slot_off(desc, sidx) + (size_t)jt * nch * 384;
+    const int tot = nch * 384;
+    constexpr int BT = (LINX_KMAX / 32 * 384 + 64 * LINX_WAVES - 1) / (64 * LINX_WAVES);
+    uint4 v[BT];
+#pragma unroll
+    for (int u = 0; u < BT; ++u) {
+      const int e = threadIdx.x + u * 64 * LINX_WAVES;
+      v[u] = src[min(e, tot - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < BT; ++u) {
+      const int e = threadIdx.x + u * 64 * LINX_WAVES;
+      if (e < tot) bs[e] = v[u];
+    }
+  }
+  __syncthreads();
+  float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
+  const int g0 = gb * LINX_WAVES * LINX_GPW, g1 = min(n_groups, g0 + LINX_WAVES * LINX_GPW);
+  switch (d) {
+    case 1: lin_fwd_x6<1, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+    case 3: lin_fwd_x6<3, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+    case 5: lin_fwd_x6<5, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+    case 7: lin_fwd_x6<7, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+    default: lin_fwd_x6<9, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+  }
+}
+
+// the weights in fragment order (eelg_linear_pack): one thread per (slot, jt, chunk, kb, lane)
+// builds the 8 weights B[k = 32c + 16kb + 8hf + t][jt*32 + j] (alpha applied, zero past n_out)
+// and writes their three bf16 parts
+__global__ __launch_bounds__(256) void lin_pack_kernel(const float* __restrict__ w, eelg_lin_desc desc,
+                                                       int nunits, uint4* __restrict__ pk) {
+  const int u = blockIdx.x * 256 + threadIdx.x;   // unit = (slot, jt, c, kb, lane): 3 pieces each
+  if (u >= nunits) return;
+  int s = 0, base = 0, ks = 0, njt = 0;
+  for (;; ++s) {
+    ks = 0;
+    for (int t = 0; t < desc.slot[s].n_src; ++t) ks += desc.slot[s].src[t].k;
+    njt = (desc.slot[s].n_out + 31) / 32;
+    const int nu = njt * (ks / 32) * 128;
+    if (u < base + nu || s + 1 >= desc.n_slots) break;
+    base += nu;
+  }
+  const eelg_lin_slot& sl = desc.slot[s];
+  const int nch = ks / 32;
+  int r = u - base;
+  const int lane = r & 63; r >>= 6;
+  const int kb = r & 1; r >>= 1;
+  const int c = r % nch, jt = r / nch;
+  const int j = jt * 32 + (lane & 31), k0 = 32 * c + 16 * kb + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    int k = k0 + t, q = 0;
+    while (k >= sl.src[q].k) { k -= sl.src[q].k; ++q; }
+    const eelg_lin_src& src = sl.src[q];
+    v[t] = j < sl.n_out ? src.alpha * w[src.w_off + (size_t)k * src.ldk + (size_t)j * src.ldj] : 0.0f;
+  }
+  uint4 p[3];
+  eelg_split8(v, p);
+  const size_t o = (size_t)lin_pack_slot_off(desc, s) + ((size_t)(jt * nch + c) * 2 + kb) * 384 + lane;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) pk[o + q * 64] = p[q];
+}

@@ -4,11 +4,16 @@
 // with w[E, n_out] the per-edge tensor-product weights (n_out = 1344 for the l>=1 layers of
 // BASELINE config 2).  The reference runs this as torch.nn.Sequential of Linear + SiLU.
 //
-// Every GEMM here is on v_mfma_f32_32x32x2_f32 (exact f32 products, fmaf-chain numerics).
-// Fragment convention (32x32x2): lane l = 32*hf + i supplies A[row i][k] and B[k][col i] for
-// the step's k; the two lane halves take k = hf*KH + st over a K block of 2*KH, i.e. the K
-// order is permuted (a sum, so any bijection shared by A and B is exact up to rounding
-// order).  C/D: acc[r] is row (r&3) + 8*(r>>2) + 4*hf, column i.
+// The hidden layers run on v_mfma_f32_32x32x2_f32 (exact f32 products).  Fragment convention
+// (32x32x2): lane l = 32*hf + i supplies A[row i][k] and B[k][col i] for the step's k; the two
+// lane halves take k = hf*KH + st over a K block of 2*KH, i.e. the K order is permuted (a sum,
+// so any bijection shared by A and B is exact up to rounding order).  The three large GEMMs
+// (the output layer and its two gradients: 64 x n_out per edge, ~93 % of the MLP's FLOPs) run
+// fp32-accurate on bf16 MFMA (v_mfma_f32_32x32x16_bf16, "x6": each fp32 operand split exactly
+// into three bf16 parts, six part products, eelg_internal.h), 3/8 of the f32 MFMA time; lane
+// (i, hf) holds A[row i][k = 8 hf + t] and B[k = 8 hf + t][col i], t = 0..7, of a K = 16 block.
+// W_o comes pre-split (eelg_split_bf16x3).  C/D of both forms: acc[r] is row
+// (r&3) + 8*(r>>2) + 4*hf, column i.
 //
 // Masked accesses are branch-free: loads of small operands read a clamped valid element and
 // select 0; the large streams go through buffer descriptors whose range check turns an
@@ -75,32 +80,28 @@ __device__ __forceinline__ int rad_row(int r, int hf) { return (r & 3) + 8 * (r 
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-#ifndef RAD_FWD_RT
-#define RAD_FWD_RT 1   // 32-edge row tiles per wave (each W_o fragment read from LDS feeds RT MFMAs)
-#endif
 template <int H, int NH, bool BF>
 __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict__ feats,
                                                          int n_edges, eelg_radial_desc d,
-                                                         const float* __restrict__ woT,
+                                                         const unsigned short* __restrict__ wop,
                                                          float* __restrict__ zsave,
                                                          void* __restrict__ out) {
-  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4, RT = RAD_FWD_RT;
-  __shared__ float hb[4 * RT * 32 * HS];
-  __shared__ float bt[2][H * 32];   // W_o^T column tile [k][j], double-buffered, shared by 4 waves
+  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4, NKB = H / 16;
+  constexpr int NBF = 3 * NKB * 64;           // B fragments (uint4) of one 32-column tile, all parts
+  constexpr int BPT = (NBF + 255) / 256;
+  __shared__ float hb[4 * 32 * HS];
+  __shared__ uint4 bt[2][NBF];                // [buf][((part * NKB + kb) * 2 + hf) * 32 + col]
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
-  const int e00 = (blockIdx.x * 4 + wave) * 32 * RT;
+  const int e0 = (blockIdx.x * 4 + wave) * 32;
   const int F = d.n_feat, W = d.n_out;
   const uint32_t E = (uint32_t)n_edges;
   const rad_rsrc_t rz = rad_rsrc(zsave, (uint32_t)NH * E * H * 4u);
   const rad_rsrc_t ro = rad_rsrc(out, E * (uint32_t)W * ES);
   const int KF = (F + 1) >> 1;  // layer 0: K = F (<= 32) split over the two lane halves
-#pragma unroll 1
-  for (int rt = 0; rt < RT; ++rt) {
-  const int e0 = e00 + 32 * rt;
-  // waves / tiles past the last edge skip the hidden layers but join the output layer's
-  // barriers (their stores fall outside the buffer range)
+  // waves past the last edge skip the hidden layers but join the output layer's barriers (their
+  // stores fall outside the buffer range)
   const bool active = e0 < n_edges;
-  float* __restrict__ hw = hb + (wave * RT + rt) * 32 * HS;
+  float* __restrict__ hw = hb + wave * 32 * HS;
   const bool rok = e0 + i < n_edges;
 
   float a[KH];
@@ -147,141 +148,147 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
         hw[row * HS + col] = rad_silu(z);
       }
   }
+  // output layer, fp32-accurate on bf16 MFMA: w[e0 + row, ct*32 + i] = sum_k h[row][k] W_o[col][k].
+  // The wave's A fragments (h, split once) stay in registers for every column tile; each
+  // 32-column tile of the split W_o (3 x 32 x H bf16) is loaded once per workgroup (coalesced
+  // 16-B pieces, the next tile in registers while the current one computes) and read by the
+  // 4 waves from LDS in fragment order.
+  uint4 ap[NKB][3];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = hw[i * HS + 16 * kb + 8 * hf + t];
+    eelg_split8(v, ap[kb]);
   }
-  // output layer: w[e0 + row, ct*32 + i], B[k][j] = W_o[j][k] = woT[k][j].  Each 32-column
-  // tile of W_o^T (H x 32 floats) is loaded once per workgroup (coalesced rows, the next tile in
-  // registers while the current one computes) and read by the 4 waves from LDS: one L2 read
-  // of W_o per 128 edges instead of per 32.
-  float ar[RT][KH];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int st = 0; st < KH; ++st) ar[rt][st] = hb[(wave * RT + rt) * 32 * HS + i * HS + hf * KH + st];
   const int nct = (W + 31) >> 5;
-  constexpr int BPT = H * 32 / 256;   // tile floats per thread
-  float rb[BPT];
+  uint4 rb[BPT];
   auto load_b = [&](int ct) {
 #pragma unroll
     for (int q = 0; q < BPT; ++q) {
-      const int e = threadIdx.x + 256 * q, k = e >> 5, col = ct * 32 + (e & 31);
-      rb[q] = rad_ld(woT, (size_t)k * W + col, col < W);
+      const int idx = threadIdx.x + 256 * q;
+      const int p = idx / (NKB * 64), rem = idx - p * (NKB * 64);
+      const int kb = rem >> 6, h2 = (rem >> 5) & 1, col = ct * 32 + (rem & 31);
+      rb[q] = (idx < NBF && col < W)
+                  ? *reinterpret_cast<const uint4*>(wop + ((size_t)p * W + col) * H + 16 * kb + 8 * h2)
+                  : make_uint4(0u, 0u, 0u, 0u);
     }
   };
   auto store_b = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < BPT; ++q) bt[buf][threadIdx.x + 256 * q] = rb[q];
+    for (int q = 0; q < BPT; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      if (idx < NBF) bt[buf][idx] = rb[q];
+    }
   };
   load_b(0);
   store_b(0);
   __syncthreads();
   for (int ct = 0; ct < nct; ++ct) {
     if (ct + 1 < nct) load_b(ct + 1);
-    const float* __restrict__ bb = bt[ct & 1] + hf * KH * 32 + i;
-    rad_f32x16 acc[RT];
+    const uint4* __restrict__ bb = bt[ct & 1] + hf * 32 + i;
+    rad_f32x16 acc;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[rt][r] = 0.0f;
+    for (int kb = 0; kb < NKB; ++kb) {
+      uint4 b[3];
 #pragma unroll
-    for (int st = 0; st < KH; ++st) {
-      const float bv = bb[st * 32];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = RAD_MFMA(ar[rt][st], bv, acc[rt]);
+      for (int p = 0; p < 3; ++p) b[p] = bb[(p * NKB + kb) * 64];
+      EELG_X6(acc, ap[kb], b);
     }
     const int col = ct * 32 + i;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint32_t off =
-            rad_off(((uint32_t)(e00 + 32 * rt + rad_row(r, hf)) * W + col) * ES, col < W);
-        if (BF)
-          rad_bst16(ro, off, eelg_f2bf(acc[rt][r]));
-        else
-          rad_bst(ro, off, acc[rt][r]);
-      }
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t off = rad_off(((uint32_t)(e0 + rad_row(r, hf)) * W + col) * ES, col < W);
+      if (BF)
+        rad_bst16(ro, off, eelg_f2bf(acc[r]));
+      else
+        rad_bst(ro, off, acc[r]);
+    }
     if (ct + 1 < nct) store_b((ct + 1) & 1);
     __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// backward 1: grad_h[E, H] = grad_w[E, W] W_o[W, H]
+// backward 1: grad_h[E, H] = grad_w[E, W] W_o[W, H]   (fp32-accurate on bf16 MFMA)
 // ---------------------------------------------------------------------------------------------
-// grad_w rows are read coalesced (4 or 8 rows x 256 B per wave-instruction) and turned into
-// the row-per-lane A layout through a wave-private LDS tile; W_o chunks are staged in LDS once
-// per workgroup and shared by its 4 waves.
+// A wave owns 32 edges; K = W runs in 32-wide chunks.  grad_w rows are read coalesced (8 or 16
+// rows x 128 B per wave-instruction) into a wave-private LDS tile, from which each lane takes its
+// A fragment (8 consecutive k of its row) and splits it; bf16 storage (config 5) is exactly one
+// bf16 part.  B[k][c] = W_o[k][c] comes from the split W_o^T ([3][H][W], k contiguous): each
+// chunk's 3 x H x 32 bf16 are staged in LDS once per workgroup in fragment order, shared by its
+// 4 waves, the next chunk's pieces in registers while the current one computes.
 template <int H, bool BF>
 __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restrict__ gw,
                                                             int n_edges, int W,
-                                                            const float* __restrict__ wo,
+                                                            const unsigned short* __restrict__ wotp,
                                                             float* __restrict__ gh) {
-  constexpr int NT = H / 32, KC = 64, ES = BF ? 2 : 4, NB = KC * H / 256;  // B floats per thread
-  constexpr int AS = KC + 4;                  // A tile row stride (floats)
-  constexpr int NV = BF ? 4 : 8;              // 16-B loads per lane per chunk
-  __shared__ float bs[2][KC * H];
+  constexpr int NT = H / 32, KC = 32, ES = BF ? 2 : 4;
+  constexpr int AS = KC + 4;                  // A tile row stride (floats; rows 16-B aligned)
+  constexpr int NV = BF ? 2 : 4;              // 16-B loads per lane per chunk
+  constexpr int NBF = 3 * NT * 2 * 64;        // B fragments per chunk: parts x col tiles x kb x lanes
+  constexpr int BPT = (NBF + 255) / 256;
+  __shared__ uint4 bs[2][NBF];                // [buf][((part * NT + ct) * 2 + kb) * 64 + hf * 32 + c]
   __shared__ float as_[4][32 * AS];
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
   const int e0 = (blockIdx.x * 4 + wave) * 32;   // waves past the last edge still stage / sync
   const uint32_t E = (uint32_t)n_edges;
   const rad_rsrc_t rg = rad_rsrc(gw, E * (uint32_t)W * ES);
-  const rad_rsrc_t rw = rad_rsrc(wo, (uint32_t)W * H * 4u);
   const rad_rsrc_t rh = rad_rsrc(gh, E * (uint32_t)H * 4u);
   const int nchunk = (W + KC - 1) / KC;
-  const bool vec = (W % (BF ? 8 : 4)) == 0;      // 16-B pieces never straddle a row end
   float* __restrict__ at = as_[wave];
 
-  // raw chunk loads, row-coalesced: fp32 piece q = rows 4q + (l >> 4), columns 4 (l & 15) ..+3;
-  // bf16 piece q = rows 8q + (l >> 3), columns 8 (l & 7) ..+7.  Rows past E read zeros.
+  // raw chunk loads, row-coalesced: fp32 piece q = rows 8q + (l >> 3), columns 4 (l & 7) ..+3;
+  // bf16 piece q = rows 16q + (l >> 2), columns 8 (l & 3) ..+7.  Rows past E and columns past W
+  // read zeros (W is a multiple of 8, so a piece is wholly in or out).
   uint4 raw[NV];
   auto load_a = [&](int kc) {
-    if (vec) {
 #pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        const int row = BF ? 8 * q + (l >> 3) : 4 * q + (l >> 4);
-        const int col = kc + (BF ? 8 * (l & 7) : 4 * (l & 15));
-        const uint32_t off = rad_off(((uint32_t)(e0 + row) * W + col) * ES, col < W);
-        raw[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)off, 0, 0));
-      }
+    for (int q = 0; q < NV; ++q) {
+      const int row = BF ? 16 * q + (l >> 2) : 8 * q + (l >> 3);
+      const int col = kc + (BF ? 8 * (l & 3) : 4 * (l & 7));
+      const uint32_t off = rad_off(((uint32_t)(e0 + row) * W + col) * ES, col < W);
+      raw[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rg, (int)off, 0, 0));
     }
   };
-  // raw -> LDS tile at[row][k - kc]; the scalar path loads straight into the tile
-  auto stage_a = [&](int kc) {
-    if (vec) {
+  auto stage_a = [&]() {
 #pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        if (BF) {
-          const int row = 8 * q + (l >> 3), c = 8 * (l & 7);
-          const uint32_t w4[4] = {raw[q].x, raw[q].y, raw[q].z, raw[q].w};
+    for (int q = 0; q < NV; ++q) {
+      if (BF) {
+        const int row = 16 * q + (l >> 2), c = 8 * (l & 3);
+        const uint32_t w4[4] = {raw[q].x, raw[q].y, raw[q].z, raw[q].w};
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            at[row * AS + c + 2 * u] = __uint_as_float(w4[u] << 16);
-            at[row * AS + c + 2 * u + 1] = __uint_as_float(w4[u] & 0xffff0000u);
-          }
-        } else {
-          const int row = 4 * q + (l >> 4), c = 4 * (l & 15);
-          *reinterpret_cast<uint4*>(&at[row * AS + c]) = raw[q];
+        for (int u = 0; u < 4; ++u) {
+          at[row * AS + c + 2 * u] = __uint_as_float(w4[u] << 16);
+          at[row * AS + c + 2 * u + 1] = __uint_as_float(w4[u] & 0xffff0000u);
         }
-      }
-    } else {
-#pragma unroll 4
-      for (int q = 0; q < 32; ++q) {
-        const int idx = l + 64 * q, row = idx >> 6, c = idx & 63;
-        const uint32_t off = rad_off(((uint32_t)(e0 + row) * W + kc + c) * ES, kc + c < W);
-        at[row * AS + c] = BF ? eelg_bf2f((unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rg, (int)off, 0, 0))
-                              : rad_bld(rg, off);
+      } else {
+        const int row = 8 * q + (l >> 3), c = 4 * (l & 7);
+        *reinterpret_cast<uint4*>(&at[row * AS + c]) = raw[q];
       }
     }
   };
-  // B: W_o rows [kc, kc + 64) are one contiguous run of 64 * H floats
-  float rb[NB];
+  uint4 rb[BPT];
   auto load_b = [&](int kc) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) rb[q] = rad_bld(rw, ((uint32_t)kc * H + threadIdx.x + 256 * q) * 4u);
+    for (int q = 0; q < BPT; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      const int c = idx & 31, h2 = (idx >> 5) & 1, kb = (idx >> 6) & 1, pc = idx >> 7;
+      const int p = pc / NT, ct = pc - p * NT;
+      const int k = kc + 16 * kb + 8 * h2;
+      rb[q] = (idx < NBF && k < W)
+                  ? *reinterpret_cast<const uint4*>(wotp + ((size_t)p * H + ct * 32 + c) * W + k)
+                  : make_uint4(0u, 0u, 0u, 0u);
+    }
   };
   auto store_b = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) bs[buf][threadIdx.x + 256 * q] = rb[q];
+    for (int q = 0; q < BPT; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      if (idx < NBF) bs[buf][idx] = rb[q];
+    }
   };
 
   rad_f32x16 acc[NT];
@@ -294,24 +301,43 @@ __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restri
   load_a(0);
   for (int c = 0; c < nchunk; ++c) {
     __syncthreads();   // chunk c staged; every wave is past chunk c-1's reads of bs[(c+1)&1]
-    // A fragments of chunk c: lane (hf, i) takes row i, k = 32 hf + st
-    stage_a(c * KC);
-    float a[32];
+    stage_a();
+    // this lane's A fragments of chunk c: row i, k = 16 kb + 8 hf + t
+    float av[2][8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(&at[i * AS + hf * 32 + 4 * q]);
-      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    for (int kb = 0; kb < 2; ++kb) {
+      const float4 v0 = *reinterpret_cast<const float4*>(&at[i * AS + 16 * kb + 8 * hf]);
+      const float4 v1 = *reinterpret_cast<const float4*>(&at[i * AS + 16 * kb + 8 * hf + 4]);
+      av[kb][0] = v0.x; av[kb][1] = v0.y; av[kb][2] = v0.z; av[kb][3] = v0.w;
+      av[kb][4] = v1.x; av[kb][5] = v1.y; av[kb][6] = v1.z; av[kb][7] = v1.w;
     }
     if (c + 1 < nchunk) {   // uniform; in flight during the MFMAs
       load_b((c + 1) * KC);
       load_a((c + 1) * KC);
     }
-    const float* __restrict__ b = bs[c & 1];
+    const uint4* __restrict__ bb = bs[c & 1] + hf * 32 + i;
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct)
+    for (int kb = 0; kb < 2; ++kb) {
+      uint4 ap[3];
+      if (BF) {
+        // exactly bf16: the high halves are the one part
+#define RAD_PK(t) __builtin_amdgcn_perm(__float_as_uint(av[kb][t + 1]), __float_as_uint(av[kb][t]), 0x07060302u)
+        ap[0] = make_uint4(RAD_PK(0), RAD_PK(2), RAD_PK(4), RAD_PK(6));
+#undef RAD_PK
+      } else {
+        eelg_split8(av[kb], ap);
+      }
 #pragma unroll
-      for (int st = 0; st < 32; ++st)
-        acc[ct] = RAD_MFMA(a[st], b[(hf * 32 + st) * H + ct * 32 + i], acc[ct]);
+      for (int ct = 0; ct < NT; ++ct) {
+        uint4 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = bb[((p * NT + ct) * 2 + kb) * 64];
+        if (BF)
+          EELG_X3(acc[ct], ap[0], b);
+        else
+          EELG_X6(acc[ct], ap, b);
+      }
+    }
     if (c + 1 < nchunk) store_b((c + 1) & 1);
   }
 #pragma unroll
@@ -457,17 +483,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAD_SMALL_W
 }
 
 // ---------------------------------------------------------------------------------------------
-// backward 3: grad of the output weight
+// backward 3: grad of the output weight   (fp32-accurate on bf16 MFMA)
 // ---------------------------------------------------------------------------------------------
-// part[s, j, k] = sum over split s's edges of grad_w[e, j] * SiLU(z_last[e, k])
+// part[s, j, k] = sum over split s's edges of grad_w[e, j] * SiLU(z_last[e, k]).  A wave owns 32
+// output rows j; K = edges in 32-edge tiles (two K = 16 blocks).  A[j][e] = grad_w[e][j]: a lane
+// loads its 16 values (coalesced over j), splits them (bf16 storage: one exact part).  B[e][k] =
+// SiLU(z_last[e][k]) is computed, split and stored in LDS in fragment order once per workgroup by
+// all its threads (one fragment per thread at H = 64), double buffered.
 template <int H, int NH, bool BF>
 __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restrict__ gw,
                                                             int n_edges, int W,
                                                             const float* __restrict__ zsave,
                                                             int tiles_per_split,
                                                             float* __restrict__ part) {
-  constexpr int HS = H + 1, NT = H / 32, ES = BF ? 2 : 4, NZ = 32 * H / 256;
-  __shared__ float hs[2][32 * HS];
+  constexpr int NT = H / 32, ES = BF ? 2 : 4;
+  constexpr int NFR = NT * 2 * 64;             // B fragments of a tile per part (ct, kb, hf, k)
+  __shared__ uint4 hs[2][3 * NFR];             // [buf][part * NFR + ((ct * 2 + kb) * 2 + hf) * 32 + k]
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
   const int j = blockIdx.x * 128 + wave * 32 + i;   // this lane's grad_w column (A row)
   const int s = blockIdx.y;
@@ -476,47 +507,73 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
   const uint32_t E = (uint32_t)n_edges;
   const rad_rsrc_t rg = rad_rsrc(gw, E * (uint32_t)W * ES);
   const rad_rsrc_t rz = rad_rsrc(zsave + (size_t)(NH - 1) * E * H, E * (uint32_t)H * 4u);
+  // the B fragment this thread builds: (ct, kb, hf, k) = decomposition of threadIdx.x
+  const bool bmine = threadIdx.x < NFR;
+  const int bk = threadIdx.x & 31, bh = (threadIdx.x >> 5) & 1, bkb = (threadIdx.x >> 6) & 1,
+            bct = threadIdx.x >> 7;
   rad_f32x16 acc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[ct][r] = 0.0f;
-  float an[16], zn[NZ];
+  float an[16], zn[8];
   auto load = [&](int t) {
-    // A[j][e] = grad_w[e][j] (32 consecutive columns per lane half); rows past E read zeros
+    // A[j][e]: e = t*32 + 16 kb + 8 hf + u; rows past E read zeros
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const uint32_t off = rad_off(((uint32_t)(t * 32 + hf * 16 + st) * W + j) * ES, j < W);
-      if (BF)
-        an[st] = eelg_bf2f((unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rg, (int)off, 0, 0));
-      else
-        an[st] = rad_bld(rg, off);
-    }
-    // z_last of the tile's 32 edges: one contiguous run of 32 * H floats
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int q = 0; q < NZ; ++q) zn[q] = rad_bld(rz, ((uint32_t)t * 32 * H + threadIdx.x + 256 * q) * 4u);
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t off = rad_off(((uint32_t)(t * 32 + 16 * kb + 8 * hf + u) * W + j) * ES, j < W);
+        if (BF)
+          an[8 * kb + u] = eelg_bf2f((unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rg, (int)off, 0, 0));
+        else
+          an[8 * kb + u] = rad_bld(rg, off);
+      }
+    // z_last[e][k] of this thread's B fragment: e = t*32 + 16 bkb + 8 bh + u, k = bct*32 + bk
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      zn[u] = rad_bld(rz, rad_off(((uint32_t)(t * 32 + 16 * bkb + 8 * bh + u) * H + bct * 32 + bk) * 4u, bmine));
   };
   if (t0 < t1) load(t0);
   for (int t = t0; t < t1; ++t) {
-    // h_last = SiLU(z_last), staged once for the 4 waves.  Double buffered: the barrier of
-    // tile t+1 separates tile t's reads of a buffer from its rewrite at tile t+2.
-    float* __restrict__ hb = hs[t & 1];
+    // h_last = SiLU(z_last) (SiLU(0) = 0 past the last edge), split, in fragment order.  Double
+    // buffered: the barrier of tile t+1 separates tile t's reads of a buffer from its rewrite.
+    uint4* __restrict__ hb = hs[t & 1];
+    if (bmine) {
+      float v[8];
 #pragma unroll
-    for (int q = 0; q < NZ; ++q) {
-      const int idx = threadIdx.x + 256 * q;
-      const int r = idx / H, c = idx - r * H;
-      hb[r * HS + c] = rad_silu(zn[q]);   // SiLU(0) = 0 past the last edge
+      for (int u = 0; u < 8; ++u) v[u] = rad_silu(zn[u]);
+      uint4 pp[3];
+      eelg_split8(v, pp);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) hb[p * NFR + threadIdx.x] = pp[p];
     }
     __syncthreads();
-    float a[16];
+    uint4 ap[2][3];
 #pragma unroll
-    for (int st = 0; st < 16; ++st) a[st] = an[st];
+    for (int kb = 0; kb < 2; ++kb) {
+      if (BF) {
+#define RAD_PK(t) __builtin_amdgcn_perm(__float_as_uint(an[8 * kb + t + 1]), __float_as_uint(an[8 * kb + t]), 0x07060302u)
+        ap[kb][0] = make_uint4(RAD_PK(0), RAD_PK(2), RAD_PK(4), RAD_PK(6));
+#undef RAD_PK
+      } else {
+        eelg_split8(&an[8 * kb], ap[kb]);
+      }
+    }
     if (t + 1 < t1) load(t + 1);   // in flight during the MFMAs
+    const uint4* __restrict__ bb = hb + hf * 32 + i;
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int st = 0; st < 16; ++st)
-        acc[ct] = RAD_MFMA(a[st], hb[(hf * 16 + st) * HS + ct * 32 + i], acc[ct]);
+      for (int kb = 0; kb < 2; ++kb) {
+        uint4 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = bb[p * NFR + (ct * 2 + kb) * 64];
+        if (BF)
+          EELG_X3(acc[ct], ap[kb][0], b);
+        else
+          EELG_X6(acc[ct], ap[kb], b);
+      }
   }
   const int jb = blockIdx.x * 128 + wave * 32;
 #pragma unroll
@@ -531,6 +588,20 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
 // ---------------------------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------------------------
+// the exact three-part bf16 split of an fp32 array (eelg_split_bf16x3): parts[p * n + i]
+__global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restrict__ src, long long n,
+                                                           unsigned short* __restrict__ parts) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float x = src[i];
+  const unsigned a = __float_as_uint(x) & 0xffff0000u;
+  const float r = x - __uint_as_float(a);
+  const unsigned b = __float_as_uint(r) & 0xffff0000u;
+  parts[i] = (unsigned short)(a >> 16);
+  parts[n + i] = (unsigned short)(b >> 16);
+  parts[2 * n + i] = (unsigned short)(__float_as_uint(r - __uint_as_float(b)) >> 16);
+}
+
 static int radial_check(const eelg_radial_desc* d, int n_edges, int out_es) {
   if (!d) return eelg_fail(-2, "radial: null descriptor");
   if (d->hidden != 32 && d->hidden != 64)
@@ -539,7 +610,9 @@ static int radial_check(const eelg_radial_desc* d, int n_edges, int out_es) {
     return eelg_fail(-2, "radial: %d hidden layers not built (1..%d)", d->n_hidden, EELG_RADIAL_MAXH);
   if (d->n_feat < 1 || d->n_feat > 32)
     return eelg_fail(-2, "radial: %d input features not built (1..32)", d->n_feat);
-  if (d->n_out < 1) return eelg_fail(-2, "radial: n_out must be positive");
+  if (d->n_out < 1 || d->n_out % 8)
+    return eelg_fail(-2, "radial: n_out %d must be a positive multiple of 8 (16-B pieces of the "
+                         "split W_o rows)", d->n_out);
   if (n_edges < 0) return eelg_fail(-2, "radial: negative edge count");
   // buffer descriptors address each stream with 32-bit byte offsets (< 2 GiB)
   const long long e = n_edges;
@@ -602,22 +675,37 @@ int eelg_radial_plan(int n_edges, int n_out, int* n_part, int* n_split) {
   return 0;
 }
 
-int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const float* wo_t,
+int eelg_split_bf16x3(const float* src, long long n, void* parts, void* stream) {
+  if (n < 0) return eelg_fail(-2, "split_bf16x3: negative length");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, src, n, static_cast<unsigned short*>(parts));
+  return eelg_check_launch("split_bf16x3");
+}
+
+static bool rad_a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const void* wo_parts,
                     int out_bf16, float* zsave, void* out, void* stream) {
   if (int rc = radial_check(d, n_edges, out_bf16 ? 2 : 4)) return rc;
+  if (!rad_a16(wo_parts)) return eelg_fail(-2, "radial_fwd: wo_parts must be 16-byte aligned");
   if (n_edges == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const bool bf = out_bf16 != 0;
-  const dim3 grid((n_edges + 128 * RAD_FWD_RT - 1) / (128 * RAD_FWD_RT));
-  RAD_LAUNCH3(radial_fwd_kernel, grid, feats, n_edges, *d, wo_t, zsave, out);
+  const dim3 grid((n_edges + 127) / 128);
+  const unsigned short* wop = static_cast<const unsigned short*>(wo_parts);
+  RAD_LAUNCH3(radial_fwd_kernel, grid, feats, n_edges, *d, wop, zsave, out);
   return eelg_check_launch("radial_fwd");
 }
 
 int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
-                    const float* wo, const float* zsave, const float* feats, float* grad_h,
+                    const void* wot_parts, const float* zsave, const float* feats, float* grad_h,
                     float* part_h, float* part_wo, void* stream) {
   if (int rc = radial_check(d, n_edges, grad_bf16 ? 2 : 4)) return rc;
+  if (!rad_a16(wot_parts) || !rad_a16(grad_w))
+    return eelg_fail(-2, "radial_bwd: grad_w and wot_parts must be 16-byte aligned");
   if (n_edges == 0) return 0;
+  const unsigned short* wotp = static_cast<const unsigned short*>(wot_parts);
   hipStream_t st = (hipStream_t)stream;
   const bool bf = grad_bf16 != 0;
   int nw, ns, tps;
@@ -625,11 +713,11 @@ int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_r
   const dim3 g1((n_edges + 127) / 128);
   const int W = d->n_out;
   if (d->hidden == 64) {
-    if (bf) hipLaunchKernelGGL((radial_bwd_gh_kernel<64, true>), g1, dim3(256), 0, st, grad_w, n_edges, W, wo, grad_h);
-    else hipLaunchKernelGGL((radial_bwd_gh_kernel<64, false>), g1, dim3(256), 0, st, grad_w, n_edges, W, wo, grad_h);
+    if (bf) hipLaunchKernelGGL((radial_bwd_gh_kernel<64, true>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
+    else hipLaunchKernelGGL((radial_bwd_gh_kernel<64, false>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
   } else {
-    if (bf) hipLaunchKernelGGL((radial_bwd_gh_kernel<32, true>), g1, dim3(256), 0, st, grad_w, n_edges, W, wo, grad_h);
-    else hipLaunchKernelGGL((radial_bwd_gh_kernel<32, false>), g1, dim3(256), 0, st, grad_w, n_edges, W, wo, grad_h);
+    if (bf) hipLaunchKernelGGL((radial_bwd_gh_kernel<32, true>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
+    else hipLaunchKernelGGL((radial_bwd_gh_kernel<32, false>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
   }
   if (int rc = eelg_check_launch("radial_bwd_gh")) return rc;
   const dim3 g2(nw);

@@ -51,14 +51,18 @@ TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
 TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
-# symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
-# computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
-# 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
-# 1 ahead, it spills SGPRs beyond)
-SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
+# symmetric contraction: terms per pinned block (a scheduling region: the pins keep hipcc from
+# hoisting the monomials of later blocks), forward / grad-x
 SC_BLOCK_FWD = int(os.environ.get("EELG_SC_BLOCK_FWD", "32"))
-SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "1"))
 SC_BLOCK_BWD = int(os.environ.get("EELG_SC_BLOCK_BWD", "64"))
+# fwd / grad-x: the coefficient stream.  Each wave's channel row of coefficients travels by
+# LDS-DMA (global_load_lds_dwordx4) in chunks of SC_CCH terms into a per-wave ring of
+# SC_CSLOTS slots; the polynomial reads them as 4-term quads (ds_read_b128, a wave-uniform
+# broadcast) SC_CD quads ahead of use.  The coefficient row stride is padded to a multiple of
+# SC_CCH (sc config coef_ld).
+SC_CCH = int(os.environ.get("EELG_SC_CCH", "128"))
+SC_CSLOTS = int(os.environ.get("EELG_SC_CSLOTS", "3"))
+SC_CD = int(os.environ.get("EELG_SC_CD", "4"))
 # fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
 # consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
 SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
@@ -991,6 +995,88 @@ def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> L
     return out
 
 
+class CoefStream:
+    """Emitter of a wave's coefficient stream (fwd / grad-x of the contraction).
+
+    Chunk k (terms [k*ch, (k+1)*ch) of the wave's channel row) is moved by ONE LDS-DMA
+    instruction (ch/4 lanes x 16 B) into ring slot k % S; the DMAs of chunks 0..S-1 are issued
+    at kernel start, and the DMA of chunk k+S once every read of chunk k has completed.  The
+    straight-line polynomial reads 4-term quads with inline-asm ds_read_b128 (wave-uniform
+    address: a broadcast) ``ahead`` quads before the quad it needs and waits with counted
+    ``s_waitcnt lgkmcnt`` (LDS reads of a wave return in order); a chunk's first read waits
+    with a counted ``s_waitcnt vmcnt`` that leaves the later chunks' DMAs in flight (vector
+    loads return in order).  The reads are asm because hipcc would otherwise order every LDS
+    read after ALL outstanding LDS-DMA (it models a DMA as writing 16 B at the slot base,
+    see DESIGN 3.3).  Each quad register is threaded through its wait ("+v") before any use."""
+
+    def __init__(self, nt: int, ch: int, slots: int, ahead: int, nwaves: int):
+        assert ch in (128, 256) and slots >= 2 and 1 <= ahead <= 12
+        self.nt, self.ch, self.S, self.D, self.NW = nt, ch, slots, ahead, nwaves
+        self.nq = (nt + 3) // 4
+        self.nchunk = -(-nt // ch)
+        self.issued = 0          # quads [0, issued) have their read issued
+        self.waited = 0          # quads [0, waited) have completed
+        self.ready = 0           # chunks [0, ready) have landed in LDS (vmcnt waited)
+        self.dmas = 0            # chunks [0, dmas) have their DMA issued
+        self.released = 0        # chunks [0, released) are fully read (slot reusable)
+
+    def decl(self) -> List[str]:
+        return [f"  __shared__ float4 cring_[{self.NW}][{self.S}][{self.ch // 4}];   // per-wave coefficient ring"]
+
+    def prologue(self) -> List[str]:
+        out = ["  const int wvu_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);",
+               "  const unsigned crb_ = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)&cring_[wvu_][0][0]);"]
+        for j0 in range(0, self.nq, 32):   # quads are assigned inside nested scopes, declared here
+            out.append("  eelg_f4r " + ", ".join(f"cq{j}" for j in range(j0, min(j0 + 32, self.nq))) + ";")
+        for _ in range(min(self.S, self.nchunk)):
+            out += self._dma()
+        return out
+
+    def _dma(self) -> List[str]:
+        k = self.dmas
+        self.dmas += 1
+        guard = "if (lane < 32) " if self.ch == 128 else ""
+        return [f"  {guard}__builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
+                f"(cf + {k * self.ch} + 4 * lane), (__attribute__((address_space(3))) void*)"
+                f"&cring_[wvu_][{k % self.S}][0], 16, 0, 0);   // coefficient chunk {k}"]
+
+    def _issue(self) -> List[str]:
+        j = self.issued
+        k = 4 * j // self.ch
+        out = []
+        if k >= self.ready:
+            assert k == self.ready and k < self.dmas
+            out.append(f'  asm volatile("s_waitcnt vmcnt({self.dmas - 1 - k})" ::: "memory");   // chunk {k} landed')
+            self.ready += 1
+        off = 4 * ((k % self.S) * self.ch + (4 * j) % self.ch)
+        out.append(f'  asm volatile("ds_read_b128 %0, %1 offset:{off}" : "=v"(cq{j}) : "v"(crb_));')
+        self.issued += 1
+        return out
+
+    def use(self, t: int) -> List[str]:
+        """lines to emit before the first use of term t"""
+        j = t // 4
+        if j < self.waited:
+            return []
+        out = []
+        while self.issued <= min(j + self.D, self.nq - 1):
+            out += self._issue()
+        done = list(range(self.waited, j + 1))
+        ops = ", ".join(f'"+v"(cq{q})' for q in done)
+        out.append(f'  asm volatile("s_waitcnt lgkmcnt({self.issued - 1 - j})" : {ops} : : "memory");')
+        self.waited = j + 1
+        # chunks whose every quad has completed: their slot takes chunk k + S
+        while self.released < self.nchunk and min(self.nq, (self.released + 1) * self.ch // 4) <= self.waited:
+            self.released += 1
+            if self.dmas < self.nchunk:
+                out += self._dma()
+        return out
+
+    @staticmethod
+    def c(t: int) -> str:
+        return f"cq{t // 4}[{t % 4}]"
+
+
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
     """Symmetric contraction kernels.
 
@@ -1030,6 +1116,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         TP += 1                             # odd -> conflict-free lane rows
     drow, orow = lin.row, lout.row
     nt = len(plan.terms)
+    cld = -(-nt // SC_CCH) * SC_CCH          # coefficient row stride: whole LDS-DMA chunks
 
     def lq(lay, a, cl):
         """LDS column of component a for channel-in-quad cl (may be a runtime expr)."""
@@ -1156,14 +1243,17 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
             f"  const int cl = __builtin_amdgcn_readfirstlane(wv & {Q - 1});",
-            f"  const float* __restrict__ cf = coef + (size_t)c * {nt};"]
+            f"  const float* __restrict__ cf = coef + (size_t)c * {cld};"]
 
     # ---------------- forward ----------------
     L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[{NB} * {TP}];")
+    cs = CoefStream(nt, SC_CCH, SC_CSLOTS, SC_CD, NTH // 64)
+    L += cs.decl()
     L += head
+    L += cs.prologue()
     L += stage_in("x", "tile", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
@@ -1173,33 +1263,30 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  float o{q} = 0.0f;")
     blocks = sc_blocks(plan, SC_BLOCK_FWD)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    for b0 in blocks[:SC_PFD_FWD]:
-        for t in b0["terms"]:
-            L.append(f"  float c{t} = cf[{t}];")
+    C = CoefStream.c
     for bi, blk in enumerate(blocks):
-        # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
-        for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
-            L.append(f"  float c{t} = cf[{t}];")
-        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
+                L += cs.use(t)
+                L.append(f"  o{q} = fmaf({C(t)}, x{a}, o{q});")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv = f"p{a}_{b}"
             if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b};")
             for t, q in sg["d2"]:
-                L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
+                L += cs.use(t)
+                L.append(f"  o{q} = fmaf({C(t)}, {pv}, o{q});")
             for cc, lst in sg["d3"]:
                 L.append(f"  {{ const float m = {pv} * x{cc};")
                 for t, q in lst:
-                    L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
+                    L += cs.use(t)
+                    L.append(f"    o{q} = fmaf({C(t)}, m, o{q});")
                 L.append("  }")
             if not sg["last"]:
                 carry = [pv]
-        L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  " + pin(fv + carry))
     L.append("  __syncthreads();")
     for q in range(Dout):
         L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
@@ -1217,7 +1304,10 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # separate x / grad_out tiles.  When xt / gt are given, the staged tiles are also written
     # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
     L.append(f"  __shared__ float tx[{NB} * {TP}];")
+    cs = CoefStream(nt, SC_CCH, SC_CSLOTS, SC_CD, NTH // 64)
+    L += cs.decl()
     L += head
+    L += cs.prologue()
     L += stage_in("x", "tx", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (xt) {")
@@ -1237,35 +1327,31 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     blocks = sc_blocks(plan, SC_BLOCK_BWD)
-    for b0 in blocks[:SC_PFD_BWD]:
-        for t in b0["terms"]:
-            L.append(f"  float c{t} = cf[{t}];")
     for bi, blk in enumerate(blocks):
-        # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
-        for t in (blocks[bi + SC_PFD_BWD]["terms"] if bi + SC_PFD_BWD < len(blocks) else []):
-            L.append(f"  float c{t} = cf[{t}];")
-        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_BWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
+                L += cs.use(t)
+                L.append(f"  d{a} = fmaf({C(t)}, g{q}, d{a});")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv, sv = f"p{a}_{b}", f"s{a}_{b}"
             if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
             for t, q in sg["d2"]:
-                L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
+                L += cs.use(t)
+                L.append(f"  {sv} = fmaf({C(t)}, g{q}, {sv});")
             for cc, lst in sg["d3"]:
                 L.append("  { float s = 0.0f;")
                 for t, q in lst:
-                    L.append(f"    s = fmaf(c{t}, g{q}, s);")
+                    L += cs.use(t)
+                    L.append(f"    s = fmaf({C(t)}, g{q}, s);")
                 L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
             if sg["last"]:
                 L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
             else:
                 carry = [pv, sv]
-        L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  " + pin(bv + carry))
     L.append("  __syncthreads();")
     for a in range(D):
         L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
@@ -1365,7 +1451,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append("  __syncthreads();")
     L.append("  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;")
-    L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {nt};")
+    L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {cld};")
     L.append(f"  for (int k = 0; k < {gpw}; ++k) {{")
     L.append(f"    const int jg = __builtin_amdgcn_readfirstlane(k * {WV} + wv);")
     L.append("    float acc[64];")
@@ -1429,7 +1515,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
-    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, njg=len(groups), wpb=WPB, nbc=NBC, nb=NB, nth=NTH,
+    info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, cld=cld, njg=len(groups), wpb=WPB, nbc=NBC, nb=NB, nth=NTH,
                 cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
@@ -1476,7 +1562,7 @@ def main(outdir: str) -> None:
     for name, i in sc_table:
         parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                      f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}}},')
+                     f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}, {i["cld"]}}},')
     parts.append("};")
     parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
     parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")

@@ -55,6 +55,10 @@ _SIGS = {
     "eelg_linear_fwd_res": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_radial_plan": ([_I, _I, _P, _P], _I),
+    "eelg_linear_pack_size": ([_P], ctypes.c_longlong),
+    "eelg_linear_pack": ([_P, _P, _P, _P], _I),
+    "eelg_linear_fwd_pk": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
+    "eelg_split_bf16x3": ([_P, ctypes.c_longlong, _P, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
 }
@@ -181,12 +185,12 @@ def _tp_info(idx: int):
 
 
 def _sc_info(idx: int):
-    info = (ctypes.c_int * 7)()
+    info = (ctypes.c_int * 8)()
     sig = ctypes.c_uint64()
     rc = load().eelg_sc_info(idx, ctypes.cast(info, _P), ctypes.cast(ctypes.byref(sig), _P))
     if rc != 0:
         return None
-    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk")
+    keys = ("D", "x_row", "out_row", "nterms", "njg", "Dout", "coef_chunk", "coef_ld")
     return dict(zip(keys, list(info))), sig.value
 
 

@@ -193,11 +193,13 @@ class SymmetricContraction(torch.nn.Module):
         return torch.cat(ws, dim=0)                     # [K_total, mul]
 
     def coefficients(self) -> torch.Tensor:
-        """[mul, nterms] = (U_sym @ W)^T with the 1.6 %-dense U_sym applied as CSR on the GPU."""
+        """(U_sym @ W)^T with the 1.6 %-dense U_sym applied as CSR on the GPU: [mul, coef_ld],
+        rows zero-padded from nterms to the kernels' coefficient stride (CPU: [mul, nterms])."""
         if self.u_sym.is_cuda:
             if getattr(self, "_u_csr", None) is None:
                 self._u_csr = ops.SparseRows(self.u_sym)
-            return ops.symcon_coefficients(self.weight_matrix(), self._u_csr)
+            return ops.symcon_coefficients(self.weight_matrix(), self._u_csr,
+                                           self._config()[1]["coef_ld"])
         return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()
 
     def forward(self, x: torch.Tensor, y: torch.Tensor = None) -> torch.Tensor:

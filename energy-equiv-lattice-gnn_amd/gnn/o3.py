@@ -24,6 +24,9 @@ from .irreps import Irreps
 # grad-W launch shape: target workgroups and a cap on the node slices (partials)
 LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
 LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "64"))
+# forward / grad-x of the eligible linears on bf16 MFMA with fp32-accurate split operands (1),
+# or on the fp32 MFMA kernels (0)
+LIN_X6 = os.environ.get("EELG_LIN_X6", "1") != "0"
 # the readout Gate as fused HIP passes (1) or torch elementwise ops (0)
 GATE_FUSED = os.environ.get("EELG_GATE_FUSED", "1") != "0"
 
@@ -128,7 +131,9 @@ class _IrrepsLinearFn(torch.autograd.Function):
 
 
 class Linear(torch.nn.Module):
-    """e3nn ``o3.Linear`` on mul-major rows; fp32-MFMA HIP kernels (``eelg_linear_*``)."""
+    """e3nn ``o3.Linear`` on mul-major rows; HIP kernels (``eelg_linear_*``): forward and grad-x
+    on bf16 MFMA with fp32-accurate split operands where the irreps qualify
+    (``eelg_linear_fwd_pk``), fp32 MFMA otherwise and for grad-W."""
 
     def __init__(self, irreps_in, irreps_out, internal_weights: bool = True,
                  shared_weights: bool = True, biases: bool = False):
@@ -231,9 +236,56 @@ class Linear(torch.nn.Module):
             e.x_off, e.k, e.g_off = self._in_off[i], self.irreps_in[i].mul, self._out_off[o]
             e.n_out, e.d, e.w_off, e.alpha = self.irreps_out[o].mul, self.irreps_in[i].ir.dim, wo, a
         self._bw_desc = wd
+        self._pk_ok = {"fwd": self._packable(self._fwd_desc), "bx": self._packable(self._bx_desc)}
+        self._pk_cache = {}
         self._bw_maxd = max([self.irreps_in[i].ir.dim for i, _ in self.instructions] or [1])
         self._bw_tiles = sum(((self.irreps_in[i].mul + 31) // 32) * ((self.irreps_out[o].mul + 31) // 32)
                              for i, o in self.instructions) or 1
+
+    @staticmethod
+    def _packable(desc) -> bool:
+        """the descriptor qualifies for eelg_linear_fwd_pk (whole 32-wide K chunks and column
+        tiles, d odd <= 9, 16-B aligned slot offsets; the row alignment is checked per call)"""
+        for s in range(desc.n_slots):
+            sl = desc.slot[s]
+            if sl.n_src == 0 or sl.n_out % 32 or sl.y_off % 4 or sl.d not in (1, 3, 5, 7, 9):
+                return False
+            if sl.bias_off >= 0 and sl.d != 1:
+                return False
+            if sum(sl.src[t].k for t in range(sl.n_src)) > 320:
+                return False
+            for t in range(sl.n_src):
+                if sl.src[t].k % 32 or sl.src[t].x_off % 4:
+                    return False
+        return True
+
+    def _packed(self, which: str, weight):
+        """split, alpha-scaled weights of descriptor ``which`` ('fwd' or 'bx') for the packed
+        kernel, rebuilt when the weight changes (cached per weight version)"""
+        from . import _lib
+        key = (weight.data_ptr(), weight._version, weight.device)
+        hit = self._pk_cache.get(which)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        desc = self._fwd_desc if which == "fwd" else self._bx_desc
+        n = int(_lib.load().eelg_linear_pack_size(ctypes.byref(desc)))
+        pk = torch.empty(3, n, device=weight.device, dtype=torch.bfloat16)
+        _lib.check(_lib.load().eelg_linear_pack(_lib.ptr(weight), ctypes.byref(desc), _lib.ptr(pk),
+                                                _lib.stream(pk)), "linear_pack")
+        self._pk_cache[which] = (key, pk)
+        return pk
+
+    def _run_pk(self, which, x, x_row, weight, bias, extra, n, out, out_row, desc) -> bool:
+        """the packed launch when eligible; False leaves the call to the fp32 kernels"""
+        from . import _lib
+        if not (LIN_X6 and self._pk_ok[which] and x.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
+                and (extra is None or extra.data_ptr() % 16 == 0)):
+            return False
+        pk = self._packed(which, weight.detach())
+        _lib.check(_lib.load().eelg_linear_fwd_pk(
+            _lib.ptr(x), x_row, _lib.ptr(pk), _lib.ptr(bias), _lib.ptr(extra), n, _lib.ptr(out),
+            out_row, ctypes.byref(desc), _lib.stream(out)), "linear_fwd_pk")
+        return True
 
     # -- launches ---------------------------------------------------------------
     def _fwd(self, x, weight, bias, residual=None):
@@ -245,6 +297,9 @@ class Linear(torch.nn.Module):
                                      or not residual.is_contiguous()):
             raise ValueError(f"residual {tuple(residual.shape)} {residual.dtype}: expected a "
                              f"contiguous float32 {tuple(y.shape)}")
+        if self._run_pk("fwd", x, self.irreps_in.dim, weight, bias, residual, n, y,
+                        self.irreps_out.dim, self._fwd_desc):
+            return y
         _lib.check(_lib.load().eelg_linear_fwd_res(
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(weight), _lib.ptr(bias), _lib.ptr(residual), n,
             _lib.ptr(y), self.irreps_out.dim, ctypes.byref(self._fwd_desc), _lib.stream(y)),
@@ -262,6 +317,9 @@ class Linear(torch.nn.Module):
             if extra.shape != gx.shape or extra.dtype != torch.float32:
                 raise ValueError(f"linear grad-x: added gradient {tuple(extra.shape)} does not "
                                  f"match {tuple(gx.shape)}")
+        if self._run_pk("bx", gy, self.irreps_out.dim, weight, None, extra, n, gx,
+                        self.irreps_in.dim, self._bx_desc):
+            return gx
         _lib.check(_lib.load().eelg_linear_fwd_res(
             _lib.ptr(gy), self.irreps_out.dim, _lib.ptr(weight), None, _lib.ptr(extra), n,
             _lib.ptr(gx), self.irreps_in.dim, ctypes.byref(self._bx_desc), _lib.stream(gx)),

@@ -408,9 +408,9 @@ def in_degree_scale(csr: EdgeCSR) -> torch.Tensor:
 class _SymCon(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int, side=None):
-        x, coef = _a16(x), _f32(coef)
+        x, coef = _a16(x), _a16(coef)
         n = x.shape[0]
-        if x.shape[1] != info["x_row"] or coef.shape != (mul, info["nterms"]):
+        if x.shape[1] != info["x_row"] or coef.shape != (mul, info["coef_ld"]):
             raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
         out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
@@ -469,7 +469,9 @@ class _SymCon(torch.autograd.Function):
                 TIMER.stop(tok)
             chunk = ctx.info["coef_chunk"]          # LDS-resident nodes per workgroup
             nch = (n + chunk - 1) // chunk
-            part = torch.empty(nch, ctx.mul, ctx.info["nterms"], device=x.device, dtype=torch.float32)
+            part = torch.empty(nch, ctx.mul, ctx.info["coef_ld"], device=x.device, dtype=torch.float32)
+            if ctx.info["coef_ld"] != ctx.info["nterms"]:
+                part[:, :, ctx.info["nterms"]:].zero_()   # the kernel writes terms < nterms
             side = ctx.side if (SC_COEF_ON_SIDE or cm_side) else None
             if side is not None:
                 # the coefficient gradient runs on the side stream, where its consumer (the
@@ -525,6 +527,17 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
                                                    dtype=acc)
 
 
+def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
+    """[3, *t.shape] bf16 parts of an fp32 tensor with t == parts.sum(0) exactly
+    (``eelg_split_bf16x3``): the operand form of the fp32-accurate bf16 MFMA GEMMs."""
+    _require_device(t)
+    t = _f32(t)
+    parts = torch.empty((3,) + tuple(t.shape), device=t.device, dtype=torch.bfloat16)
+    _lib.check(_lib.load().eelg_split_bf16x3(_lib.ptr(t), t.numel(), _lib.ptr(parts),
+                                             _lib.stream(parts)), "split_bf16x3")
+    return parts
+
+
 def _radial_desc(params, n_feat: int):
     n_hidden = (len(params) - 1) // 2
     hidden = params[0].shape[0]
@@ -550,8 +563,9 @@ def _radial_chunks(e: int, n_out: int, out_es: int, hidden: int, n_hidden: int):
 
 class _RadialMLP(torch.autograd.Function):
     """Linear(+bias)-SiLU-...-Linear(no bias) on edge features as one fused HIP kernel
-    (``eelg_radial_fwd``: fp32 MFMA, hidden activations in LDS, only the pre-activations
-    and the [E, W] output reach HBM), backward as two (``eelg_radial_bwd``).  No grad w.r.t.
+    (``eelg_radial_fwd``: hidden layers on fp32 MFMA, the output layer fp32-accurate on bf16
+    MFMA with split operands, hidden activations in LDS, only the pre-activations and the
+    [E, W] output reach HBM), backward as three (``eelg_radial_bwd``).  No grad w.r.t.
     the features, which come from eelg_edge_embed without grad.  Edge sets past
     the kernels' 2 GiB per-stream limit run as several launches (``_radial_chunks``)."""
 
@@ -565,31 +579,48 @@ class _RadialMLP(torch.autograd.Function):
         wo = params[-1]
         if wo.shape[1] != d.hidden or any(p.shape[0] != d.hidden for p in params[:-1]):
             raise ValueError("radial MLP: hidden widths differ between layers")
-        out = torch.empty(e, d.n_out, device=feats.device, dtype=out_dtype)
-        wo_t = wo.t().contiguous()
+        # the kernels take the output width in whole 16-B pieces of bf16 (a multiple of 8, as every
+        # generated TP weight count is); another width runs on zero-padded W_o rows
+        n_out = d.n_out
+        wp = -(-n_out // 8) * 8
+        if wp != n_out:
+            wo = torch.cat([wo, wo.new_zeros(wp - n_out, wo.shape[1])])
+            d.n_out = wp
+        out = torch.empty(e, wp, device=feats.device, dtype=out_dtype)
+        wo_parts = split_bf16x3(wo)                  # [3, n_out, hidden]: the output layer's B operand
         lib = _lib.load()
         chunks = _radial_chunks(e, d.n_out, out.element_size(), d.hidden, d.n_hidden)
         zs = []
         for a, b in chunks:
             z = torch.empty(d.n_hidden, b - a, d.hidden, device=feats.device, dtype=torch.float32)
             _lib.check(lib.eelg_radial_fwd(_lib.ptr(feats[a:b]), b - a, ctypes.byref(d),
-                                           _lib.ptr(wo_t), int(out_dtype == torch.bfloat16),
+                                           _lib.ptr(wo_parts), int(out_dtype == torch.bfloat16),
                                            _lib.ptr(z), _lib.ptr(out[a:b]), _lib.stream(feats)),
                        "radial_fwd")
             zs.append(z)
         ctx.chunks = chunks
         ctx.save_for_backward(feats, *params, *zs)
         ctx.n_params = len(params)
-        return out
+        return out if wp == n_out else out[:, :n_out]
 
     @staticmethod
     def backward(ctx, g):
         feats, *rest = ctx.saved_tensors
         params, zs = rest[:ctx.n_params], rest[ctx.n_params:]
-        g = g.contiguous()
         e, nf = feats.shape
         d = _radial_desc(params, nf)
+        n_out = d.n_out
+        wp = -(-n_out // 8) * 8
+        wo = params[-1]
+        if wp != n_out:                                            # zero-padded width (forward)
+            wo = torch.cat([wo, wo.new_zeros(wp - n_out, wo.shape[1])])
+            g = torch.cat([g, g.new_zeros(g.shape[0], wp - n_out)], 1)
+            d.n_out = wp
+        g = g.contiguous()
+        if g.data_ptr() % 16:
+            g = g.clone()
         lib = _lib.load()
+        wot_parts = split_bf16x3(wo.t().contiguous())             # [3, hidden, n_out]
         h = d.hidden
         n_small = h * nf + h + (d.n_hidden - 1) * (h * h + h)
         small, gwo = None, None
@@ -605,7 +636,7 @@ class _RadialMLP(torch.autograd.Function):
                 part_h.zero_()
                 part_wo.zero_()
             _lib.check(lib.eelg_radial_bwd(_lib.ptr(g[a:b]), int(g.dtype == torch.bfloat16), ec,
-                                           ctypes.byref(d), _lib.ptr(params[-1]), _lib.ptr(z),
+                                           ctypes.byref(d), _lib.ptr(wot_parts), _lib.ptr(z),
                                            _lib.ptr(feats[a:b]), _lib.ptr(grad_h), _lib.ptr(part_h),
                                            _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
             sm, wo = part_h.sum(0), part_wo.sum(0)
@@ -615,7 +646,7 @@ class _RadialMLP(torch.autograd.Function):
         for p in params[:-1]:
             grads.append(small[off: off + p.numel()].view_as(p))
             off += p.numel()
-        grads.append(gwo)
+        grads.append(gwo if wp == n_out else gwo[:n_out].contiguous())
         return (None, None, *grads)
 
 
@@ -673,17 +704,20 @@ def _spmm(trip, n_rows, B, ldb_r, ldb_c, n_cols, out, ldo_r, ldo_c):
 
 
 class _SymConCoef(torch.autograd.Function):
-    """coef[c, t] = sum_k U[t, k] W[k, c]  ([mul, nterms], the layout the sc kernels read)."""
+    """coef[c, t] = sum_k U[t, k] W[k, c]  ([mul, ld], the layout the sc kernels read: rows
+    padded to ``ld`` >= nterms, the padding zero)."""
 
     @staticmethod
-    def forward(ctx, w, sp: SparseRows):
+    def forward(ctx, w, sp: SparseRows, ld: int):
         _require_device(w)
         w = _f32(w)
         nt, nk = sp.shape
         mul = w.shape[1]
         a, t = sp.on(w.device)
-        coef = torch.empty(mul, nt, device=w.device, dtype=torch.float32)
-        _spmm(a, nt, w, mul, 1, mul, coef, 1, nt)                 # out[t, c] at c*nt + t
+        coef = torch.empty(mul, ld, device=w.device, dtype=torch.float32)
+        if ld != nt:
+            coef[:, nt:].zero_()
+        _spmm(a, nt, w, mul, 1, mul, coef, 1, ld)                 # out[t, c] at c*ld + t
         ctx.sp, ctx.mul = sp, mul
         return coef
 
@@ -693,11 +727,12 @@ class _SymConCoef(torch.autograd.Function):
         sp, mul = ctx.sp, ctx.mul
         nt, nk = sp.shape
         a, t = sp.on(g.device)
-        gt = g.t().contiguous()                                   # [nt, mul]: coalesced over c
+        gt = g.t().contiguous()                                   # [ld, mul]: coalesced over c
         gw = torch.empty(nk, mul, device=g.device, dtype=torch.float32)
-        _spmm(t, nk, gt, mul, 1, mul, gw, mul, 1)
-        return gw, None
+        _spmm(t, nk, gt, mul, 1, mul, gw, mul, 1)                 # reads rows t < nterms only
+        return gw, None, None
 
 
-def symcon_coefficients(w: torch.Tensor, sp: SparseRows) -> torch.Tensor:
-    return _SymConCoef.apply(w, sp)
+def symcon_coefficients(w: torch.Tensor, sp: SparseRows, ld: Optional[int] = None) -> torch.Tensor:
+    """[mul, ld] coefficients (``ld``: the contraction config's ``coef_ld``; default nterms)."""
+    return _SymConCoef.apply(w, sp, sp.shape[0] if ld is None else ld)

@@ -36,12 +36,13 @@ const char* eelg_last_error(void);
  * sig is a structural hash the host re-derives to detect a stale build. */
 int eelg_tp_find(const char* name);
 int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
-/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk}
+/* info receives {D, x_row, out_row, nterms, n_term_groups, D_out, coef_chunk, coef_ld}
  * (D: coupling components per channel of the input, D_out: of the output; they differ when the
  * product maps the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node
- * chunk of eelg_sc_bwd_coef) */
+ * chunk of eelg_sc_bwd_coef; coef_ld: the row stride of the coefficient matrix, nterms rounded
+ * up to the kernels' coefficient DMA chunk, a multiple of 128) */
 int eelg_sc_find(const char* name);
-int eelg_sc_info(int cfg, int* info7, uint64_t* sig);
+int eelg_sc_info(int cfg, int* info8, uint64_t* sig);
 
 /* Edge geometry + embeddings.
  * Replaces get_edge_vectors_and_lengths (gnn/mace.py:338-352),
@@ -187,8 +188,10 @@ int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_row
 
 /* Symmetric contraction (correlation 3) as a sparse polynomial per (node, channel).
  * Replaces SymmetricContraction.forward (gnn/mace.py:173-177, 242-277).
- * x, out: [N, mul*D] mul-major rows; coef: [mul, nterms].  The row tensors (x, out, grad_out,
- * grad_x) must be 16-byte aligned (float4 row access); a misaligned pointer returns -2. */
+ * x, out: [N, mul*D] mul-major rows; coef: [mul, coef_ld] (info[7]; entries past nterms are
+ * read but unused), 16-byte aligned: each wave streams its channel's row into LDS by LDS-DMA in
+ * 16-B pieces.  The row tensors (x, out, grad_out, grad_x) must be 16-byte aligned (float4 row
+ * access); a misaligned pointer returns -2. */
 int eelg_sc_fwd(int cfg, const float* x, const float* coef, int n_nodes, int mul, float* out,
                 void* stream);
 int eelg_sc_bwd_x(int cfg, const float* x, const float* coef, const float* grad_out, int n_nodes,
@@ -204,7 +207,8 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
                    void* stream);
 /* Coefficient gradient (replaces the weight gradient through the U.W contraction of
  * gnn/mace.py:242-277) from the channel-major copies xt[(c*D + a)*N + n] / gt of x and
- * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_chunks, mul, nterms],
+ * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_chunks, mul, coef_ld] (the
+ * entries past nterms of each row are not written),
  * n_chunks = ceil(n_nodes / chunk); chunk must be the config's coef_chunk (info[6]): one
  * workgroup keeps that many nodes of one channel resident in LDS.  The caller sums over
  * chunks (deterministic). */
@@ -230,6 +234,20 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
                         const float* res, int n_nodes, float* y, int y_row,
                         const eelg_lin_desc* desc, void* stream);
 
+/* The same linear on bf16 MFMA with fp32-accurate split operands (three exact bf16 parts of
+ * every fp32 operand, six part products accumulated in fp32).  The weights come
+ * pre-split by eelg_linear_pack for this descriptor: pack = bf16 [3][P], P =
+ * eelg_linear_pack_size(desc) = sum over slots of n_out * (summed source K), entry
+ * [p][off_slot + j*K_slot + k] = part p of alpha * W[k][j] (ldk / ldj of the descriptor, so a
+ * grad-x descriptor packs W^T).  The packed path needs every slot to have whole 32-wide K
+ * chunks and column tiles, d in {1,3,5,7,9} and 16-byte aligned rows / pack / res; else -2.
+ * Replaces the same o3.Linear calls as eelg_linear_fwd_res. */
+long long eelg_linear_pack_size(const eelg_lin_desc* desc);
+int eelg_linear_pack(const float* w, const eelg_lin_desc* desc, void* pack, void* stream);
+int eelg_linear_fwd_pk(const float* x, int x_row, const void* pack, const float* bias,
+                       const float* res, int n_nodes, float* y, int y_row,
+                       const eelg_lin_desc* desc, void* stream);
+
 /* grad of the weights: partial[p, w_off + u*n_out + j] over node slices p of
  * nodes_per_slice nodes (sum over p on the caller side; deterministic).
  * n_partial must be >= ceil(n_nodes / nodes_per_slice). */
@@ -243,30 +261,37 @@ int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int 
 /* Radial MLP of the interaction block, fused (gnn/blocks.py:537-549, applied at :590):
  *   [Linear(n_feat -> hidden) + SiLU] + ([Linear(hidden -> hidden) + SiLU]) * (n_hidden - 1)
  *   + Linear(hidden -> n_out, no bias)
- * on edge features feats[E, n_feat], fp32 MFMA throughout.  Built for hidden 32 / 64,
- * n_hidden 1..3, n_feat <= 32 (the reference default is 12 -> 64 -> 64 -> weight_numel).
- * w / b: the hidden Linear weights [hidden, in] and biases [hidden] in torch layout.
- * Forward: out[E, n_out] (fp32, or bf16 bit patterns when out_bf16) and the pre-activations
- * zsave[n_hidden, E, hidden] (the backward's operand); wo_t = W_o^T [hidden, n_out]. */
+ * on edge features feats[E, n_feat].  The hidden layers run on fp32 MFMA; the output layer and
+ * its gradients on bf16 MFMA with fp32-accurate operand splitting (each fp32 operand = three
+ * bf16 parts exactly, six part products accumulated in fp32; eelg_split_bf16x3).  Built for
+ * hidden 32 / 64, n_hidden 1..3, n_feat <= 32, n_out a multiple of 8 (the reference default is
+ * 12 -> 64 -> 64 -> weight_numel).  w / b: the hidden Linear weights [hidden, in] and biases
+ * [hidden] in torch layout.  Forward: out[E, n_out] (fp32, or bf16 bit patterns when out_bf16)
+ * and the pre-activations zsave[n_hidden, E, hidden] (the backward's operand); wo_parts =
+ * eelg_split_bf16x3 of W_o [n_out, hidden] (bf16 [3][n_out][hidden], 16-byte aligned). */
 #define EELG_RADIAL_MAXH 3
 typedef struct {
   int n_feat, hidden, n_hidden, n_out;
   const float* w[EELG_RADIAL_MAXH];
   const float* b[EELG_RADIAL_MAXH];
 } eelg_radial_desc;
-int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const float* wo_t,
+int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, const void* wo_parts,
                     int out_bf16, float* zsave, void* out, void* stream);
+/* parts[p*n + i] (bf16 bit patterns, p = 0..2): src[i] = parts[i] + parts[n+i] + parts[2n+i]
+ * exactly (truncation split: the top 8 significant bits, the next 8, the rest). */
+int eelg_split_bf16x3(const float* src, long long n, void* parts, void* stream);
 /* Partial-buffer sizes of eelg_radial_bwd for E edges: part_h has n_part rows of
  * hidden*n_feat + hidden + (n_hidden-1)*(hidden^2 + hidden) floats (grad W_0, grad b_0, grad W_1,
  * ... in torch layout); part_wo is [n_split, n_out, hidden]. */
 int eelg_radial_plan(int n_edges, int n_out, int* n_part, int* n_split);
-/* Backward from grad_w[E, n_out] (fp32, or bf16 when grad_bf16; wo = W_o [n_out, hidden]):
+/* Backward from grad_w[E, n_out] (fp32, or bf16 when grad_bf16; 16-byte aligned); wot_parts =
+ * eelg_split_bf16x3 of W_o^T [hidden, n_out] (bf16 [3][hidden][n_out]):
  * per-wave / per-split partials of every weight and bias gradient; the caller sums part_h
  * and part_wo over their first axis (deterministic).  grad_h[E, hidden] is workspace (it
  * receives grad_w W_o).  No gradient w.r.t. feats (the reference's edge features carry
  * none). */
 int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
-                    const float* wo, const float* zsave, const float* feats, float* grad_h,
+                    const void* wot_parts, const float* zsave, const float* feats, float* grad_h,
                     float* part_h, float* part_wo, void* stream);
 
 #ifdef __cplusplus

@@ -105,8 +105,12 @@ def test_symcon_sparse_coefficients_and_grad():
     u = sc.u_sym.double().cpu()
     wm = sc.weight_matrix().detach().double().cpu()
     ref = (u @ wm).t()
-    assert rel_err(coef, ref) < 1e-6
-    gw = u.t() @ g.double().cpu().t()                           # d/dW of sum(coef * g)
+    nt = u.shape[0]
+    # rows padded to the kernels' coefficient stride (coef_ld), the padding zero
+    assert coef.shape == (32, sc._config()[1]["coef_ld"]) and coef.shape[1] % 128 == 0
+    assert torch.equal(coef[:, nt:], torch.zeros_like(coef[:, nt:]))
+    assert rel_err(coef[:, :nt], ref) < 1e-6
+    gw = u.t() @ g[:, :nt].double().cpu().t()                   # d/dW of sum(coef * g)
     got = torch.cat([p.grad.reshape(-1) for p in sc.parameters()])
     wm_params = sc.weight_matrix()                               # same parameter order
     ws = torch.autograd.grad(wm_params, list(sc.parameters()), gw.to(DEV).float())
@@ -444,11 +448,11 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
     xt, gt = cmajor(x), cmajor(g)
     ops_x, ops_g = xt, gt
     nch = -(-n // chunk)
-    part = torch.full((nch, 32, nt), float("nan"), device=DEV)
+    part = torch.full((nch, 32, info["coef_ld"]), float("nan"), device=DEV)
     lib = _lib.load()
     _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(ops_x), _lib.ptr(ops_g), n, 32, chunk, _lib.ptr(part),
                                     _lib.stream(part)), "sc_bwd_coef")
-    got = part.sum(0)
+    got = part.sum(0)[:, :nt]
     # wrong chunk sizes are rejected, not silently mis-tiled
     with pytest.raises(_lib.EELGError):
         _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(ops_x), _lib.ptr(ops_g), n, 32, chunk * 2,
@@ -538,3 +542,45 @@ def test_model_global_reductions_match_oracle(reduce):
     assert rel_err(cm, co) < 1e-4
     assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
     assert worst < 1e-5
+
+
+@pytest.mark.parametrize("irreps_in,irreps_out", [
+    ("160x0e+256x1o+320x2e+320x3o+288x4e", "32x0e+32x1o+32x2e+32x3o+32x4e"),   # the 7360 -> 800 linear
+    ("32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+32x1o+32x2e+32x3o+32x4e"),
+])
+def test_linear_packed_split_path_is_fp32_accurate(irreps_in, irreps_out):
+    """Forward and grad-x of the eligible linears run on bf16 MFMA with fp32-accurate split
+    operands (``eelg_linear_fwd_pk``).  Against the fp64 oracle their error is that of the fp32
+    MFMA kernels (``EELG_LIN_X6=0``) within 1.5x (plus 1e-7 of scale), and the packed path is the
+    one taken (its weight pack is cached)."""
+    from gnn import o3
+    torch.manual_seed(5)
+    o = oo3.Linear(irreps_in, irreps_out).double()
+    m = o3.Linear(irreps_in, irreps_out).to(DEV)
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            p.copy_(dict(o.named_parameters())[k].float())
+    n = 3001
+    x = torch.randn(n, o.irreps_in.dim, dtype=torch.float64)
+    xo = x.clone().requires_grad_(True)
+    yo = o(xo)
+    g = torch.randn_like(yo)
+    (yo * g).sum().backward()
+    errs = {}
+    saved = o3.LIN_X6
+    try:
+        for flag in (True, False):
+            o3.LIN_X6 = flag
+            m._pk_cache.clear()
+            xm = x.float().to(DEV).requires_grad_(True)
+            ym = m(xm)
+            (ym * g.float().to(DEV)).sum().backward()
+            torch.cuda.synchronize()
+            errs[flag] = (rel_err(ym, yo), rel_err(xm.grad, xo.grad))
+            if flag:
+                assert set(m._pk_cache) == {"fwd", "bx"}
+    finally:
+        o3.LIN_X6 = saved
+    record_parity(f"linear_x6_{o.irreps_in.dim}", x6=errs[True], f32=errs[False])
+    for a, b in zip(errs[True], errs[False]):
+        assert a <= 1.5 * b + 1e-7, errs

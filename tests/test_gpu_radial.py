@@ -105,3 +105,45 @@ def test_radial_mlp_deterministic():
         outs.append([y.detach().clone()] + [p.grad.clone() for p in dev.parameters()])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_split_bf16x3_is_exact():
+    """``eelg_split_bf16x3``: three bf16 parts whose sum is the fp32 input bit for bit (normal
+    range, both signs, zeros), the operand form of the fp32-accurate bf16 MFMA GEMMs."""
+    from gnn import ops
+    torch.manual_seed(3)
+    x = torch.randn(100003, device=DEV) * torch.logspace(-20, 20, 100003, device=DEV)
+    x[:7] = torch.tensor([0.0, -0.0, 1.0, -1.0, 3.0000002, 1e-30, -7.1e20], device=DEV)
+    p = ops.split_bf16x3(x)
+    assert p.dtype == torch.bfloat16 and p.shape == (3,) + x.shape
+    back = (p[0].float() + p[1].float()) + p[2].float()      # each partial sum is exact
+    assert torch.equal(back, x)
+
+
+@pytest.mark.parametrize("hidden,n_out", [(64, 1344), (32, 160)])
+def test_radial_split_gemm_as_accurate_as_fp32(hidden, n_out):
+    """The output layer and its gradients run on bf16 MFMA with split operands (six part
+    products, fp32 accumulation).  Against fp64, their error must be that of fp32 arithmetic:
+    at most 1.5x the error of the same MLP evaluated by torch in fp32 on the device (plus
+    1e-7 of the output scale), forward and every weight gradient."""
+    from gnn import ops
+    n_edges = 8192
+    ref = _mlp(12, hidden, 3, n_out, seed=11).double()
+    dev = _mlp(12, hidden, 3, n_out, seed=11).to(DEV)
+    f32 = _mlp(12, hidden, 3, n_out, seed=11).to(DEV)
+    torch.manual_seed(2)
+    feats = torch.rand(n_edges, 12, dtype=torch.float64) * 0.9
+    g = torch.randn(n_edges, n_out, dtype=torch.float64)
+    yr = ref(feats)
+    (yr * g).sum().backward()
+    yd = ops.radial_mlp(feats.float().to(DEV), dev)
+    (yd * g.float().to(DEV)).sum().backward()
+    yf = f32(feats.float().to(DEV))
+    (yf * g.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    e_split, e_f32 = rel_err(yd, yr), rel_err(yf, yr)
+    assert e_split <= 1.5 * e_f32 + 1e-7, (e_split, e_f32)
+    pr, pf = dict(ref.named_parameters()), dict(f32.named_parameters())
+    for name, p in dev.named_parameters():
+        es, ef = rel_err(p.grad, pr[name].grad), rel_err(pf[name].grad, pr[name].grad)
+        assert es <= 1.5 * ef + 1e-7, (name, es, ef)

@@ -160,7 +160,7 @@ def main():
     ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream(x)), "cm")
     chunk = sinfo["coef_chunk"]                                     # as gnn/ops.py
     nch = (n + chunk - 1) // chunk
-    part = torch.empty(nch, 32, nt, device=dev)
+    part = torch.empty(nch, 32, sinfo["coef_ld"], device=dev)
 
     def scbc():
         ops._lib.check(lib.eelg_sc_bwd_coef(sidx, ops._lib.ptr(xt), ops._lib.ptr(gt), n, 32, chunk,

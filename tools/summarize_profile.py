@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Turn a tools/profile_round.sh output dir into the committed evidence under profiles/.
 
-  python tools/summarize_profile.py gpurun_out/r01a r01a
+  python tools/summarize_profile.py gpurun_out/r01a r01a [workload-key]
 
 writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_summary.md         top kernels per step + bench line + PMC traffic table
-  profiles/pmc_traffic.json         per-kernel mean FETCH_SIZE / WRITE_SIZE bytes per launch
+  profiles/pmc_traffic.json         per-kernel mean FETCH_SIZE / WRITE_SIZE bytes per launch, under
+                                    the bench workload key (bench.workload_key; default: config 2)
 
 Counter units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  gfx950 calibration
 (profiles/r02_fetch_calibration.md, tools/proto/fetch_calib.hip): reading 1 GiB once reports
@@ -24,7 +25,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(src, tag):
+DEFAULT_WK = "egnn_b32_n1024_e4096_L4_lmax4_float32"
+
+
+def main(src, tag, wk=DEFAULT_WK):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
@@ -65,10 +69,13 @@ def main(src, tag):
         lines.append(f"| `{k[:60]}` | {g} | {t.get('FETCH_SIZE', 0)/1e6:.1f} | {2 * t.get('FETCH_SIZE', 0)/1e6:.1f} | "
                      f"{t.get('WRITE_SIZE', 0)/1e6:.1f} |")
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"source": tag, "unit": "bytes per launch", "kernels": traffic},
-              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+    path = os.path.join(prof, "pmc_traffic.json")
+    tab = json.load(open(path)) if os.path.exists(path) else {"unit": "bytes per launch", "workloads": {}}
+    if traffic:
+        tab["workloads"][wk] = {"source": tag, "kernels": traffic}
+        json.dump(tab, open(path, "w"), indent=1, sort_keys=True)
     print("\n".join(lines[:40]))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
