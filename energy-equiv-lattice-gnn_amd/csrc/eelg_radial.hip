@@ -357,6 +357,9 @@ __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restri
 // the bias gradient.  grad_h of the layer below is gz W_n, per wave on its own rows.
 // part[block, :] = this workgroup's partial of [grad W_0 (H x F), grad b_0 (H),
 //                                              grad W_1 (H x H), grad b_1, ...] (torch layout)
+#ifndef RAD_S2_H64N2
+#define RAD_S2_H64N2 0   // hidden 64, 2 hidden layers (the reference default): the LDS-quadrant kernel
+#endif
 #ifndef RAD_SMALL_WPE
 #define RAD_SMALL_WPE 2   // 2 waves/SIMD with a few spilled registers: 0.70 vs 0.90 ms for the whole backward
 #endif
@@ -478,6 +481,180 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAD_SMALL_W
     }
     off += (size_t)H * din;
     if (threadIdx.x < H) dst[off + threadIdx.x] = bacc[n];
+    off += H;
+  }
+}
+
+// backward 2, register form (hidden 64 with up to 2 hidden layers, hidden 32 with up to 3: the
+// weight-gradient accumulators fit in registers).  A wave owns whole 32-edge tiles (grid-stride)
+// and keeps every tile in the MFMA C layout (rows = edges in registers, column = lane): for
+// grad W_n = sum_e gz[e]^T h_n[e] the K axis is the edges, so with the K order permuted to
+// the C rows (step st takes edges rad_row(st, 0) and rad_row(st, 1)) both operands ARE the
+// C-layout registers of gz and h_n -- no LDS staging, no workgroup barrier per tile.  Only the
+// chain to the layer below (gz W_n, K = the hidden units) goes through a wave-private LDS
+// transpose.  The 4 waves' accumulators are summed through LDS once, at the end.
+// waves per SIMD: 2 (256 registers) where the accumulators fit, else 1 (hidden 64 with 2 hidden
+// layers: 96 accumulator registers + the tile's; EELG build flag RAD_S2_H64N2 picks the kernel)
+template <int H, int NH>
+constexpr int rad_s2_wpe() { return (H == 64 && NH >= 2) ? 1 : 2; }
+template <int H, int NH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rad_s2_wpe<H, NH>()))) void radial_bwd_small2_kernel(
+    const float* __restrict__ ghin, int n_edges, eelg_radial_desc d, const float* __restrict__ zsave,
+    const float* __restrict__ feats, float* __restrict__ part) {
+  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, NHM = NH > 1 ? NH - 1 : 1;
+  __shared__ float G[4 * 32 * HS];
+  __shared__ float WS[NHM * H * H];   // the hidden layers' weights W_1.. (the chain's B operand)
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
+  const int F = d.n_feat;
+  const int ntile = (n_edges + 31) >> 5;
+  float* __restrict__ gw_ = G + wave * 32 * HS;
+  // buffer loads with 32-bit offsets (rows past E read 0): a 64-bit address per load position,
+  // hoisted out of the tile loop, would take ~100 registers
+  const uint32_t E32 = (uint32_t)n_edges;
+  const rad_rsrc_t rgh = rad_rsrc(ghin, E32 * H * 4u);
+  const rad_rsrc_t rzs = rad_rsrc(zsave, (uint32_t)NH * E32 * H * 4u);
+  const rad_rsrc_t rft = rad_rsrc(feats, E32 * (uint32_t)F * 4u);
+#pragma unroll
+  for (int n = 1; n < NH; ++n)
+    for (int e = threadIdx.x; e < H * H; e += 256) WS[(n - 1) * H * H + e] = d.w[n][e];
+  __syncthreads();
+  rad_f32x16 accH[NHM][NT][NT], acc0[NT];
+  float bacc[NH][NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[a][r] = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NHM; ++n)
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accH[n][a][b][r] = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NH; ++n) bacc[n][a] = 0.0f;
+  }
+  for (int t = blockIdx.x * 4 + wave; t < ntile; t += gridDim.x * 4) {
+    const int e0 = t * 32;
+    rad_f32x16 gh[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = e0 + rad_row(r, hf);
+        gh[ct][r] = rad_bld(rgh, rad_off(((uint32_t)row * H + ct * 32 + i) * 4u, row < n_edges));
+      }
+#pragma unroll
+    for (int n = NH - 1; n >= 0; --n) {
+      // scheduling fences between the layers: the loads of a layer are not hoisted above the
+      // previous layer's MFMAs (their registers would stay live across them and spill)
+      __builtin_amdgcn_sched_barrier(0);
+      // gz = grad_h * SiLU'(z_n), in place (C layout)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = e0 + rad_row(r, hf);
+          const float z = rad_bld(rzs, rad_off((((uint32_t)n * E32 + row) * H + ct * 32 + i) * 4u, row < n_edges));
+          gh[ct][r] = rad_silu_grad(z, gh[ct][r]);
+        }
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        float sb = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sb += gh[ct][r];
+        bacc[n][ct] += sb;
+      }
+      if (n == 0) {
+        // grad W_0[j][k] += sum_e gz[e][j] feats[e][k], k < F <= 32 (one column tile)
+        rad_f32x16 xr;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = e0 + rad_row(r, hf);
+          xr[r] = rad_bld(rft, rad_off(((uint32_t)row * F + i) * 4u, row < n_edges && i < F));
+        }
+#pragma unroll
+        for (int jt = 0; jt < NT; ++jt)
+#pragma unroll
+          for (int st = 0; st < 16; ++st) acc0[jt] = RAD_MFMA(gh[jt][st], xr[st], acc0[jt]);
+      } else {
+        // the layer input h_n = SiLU(z_{n-1}) in C layout; grad W_n[j][c] += sum_e gz[e][j] h_n[e][c]
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {   // one column tile of h_n at a time (registers)
+          rad_f32x16 xr;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = e0 + rad_row(r, hf);
+            xr[r] = rad_silu(rad_bld(rzs, rad_off((((uint32_t)(n - 1) * E32 + row) * H + ct * 32 + i) * 4u, row < n_edges)));
+          }
+#pragma unroll
+          for (int jt = 0; jt < NT; ++jt)
+#pragma unroll
+            for (int st = 0; st < 16; ++st)
+              accH[n - 1][jt][ct] = RAD_MFMA(gh[jt][st], xr[st], accH[n - 1][jt][ct]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // grad of h_n for the layer below: gh[e][c] = sum_j gz[e][j] W_n[j][c] (rows e on the
+        // lanes: through the wave's LDS transpose)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gw_[rad_row(r, hf) * HS + ct * 32 + i] = gh[ct][r];
+        __builtin_amdgcn_wave_barrier();
+        float a3[KH];
+#pragma unroll
+        for (int st = 0; st < KH; ++st) a3[st] = gw_[i * HS + hf * KH + st];
+        __builtin_amdgcn_wave_barrier();
+        const float* __restrict__ wn = WS + (n - 1) * H * H;
+#pragma unroll
+        for (int c2 = 0; c2 < NT; ++c2) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gh[c2][r] = 0.0f;
+#pragma unroll
+          for (int st = 0; st < KH; ++st)
+            gh[c2] = RAD_MFMA(a3[st], wn[(hf * KH + st) * H + c2 * 32 + i], gh[c2]);
+        }
+      }
+    }
+  }
+  // the workgroup's partial: the 4 waves' accumulator tiles summed through LDS, one tile at a time
+  float* __restrict__ dst = part + (size_t)blockIdx.x * (size_t)((H * F + H) + (NH - 1) * (H * H + H));
+  auto reduce_tile = [&](const rad_f32x16& v, float* out, int ldo, int jb, int cb, int cmax) {
+    __syncthreads();
+    if (wave > 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) G[((wave - 1) * 16 + r) * 64 + l] = v[r];
+    __syncthreads();
+    if (wave == 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float s = v[r] + G[r * 64 + l] + G[(16 + r) * 64 + l] + G[(32 + r) * 64 + l];
+        if (cb + i < cmax) out[(size_t)(jb + rad_row(r, hf)) * ldo + cb + i] = s;
+      }
+  };
+  size_t off = 0;
+#pragma unroll
+  for (int n = 0; n < NH; ++n) {
+    const int din = n == 0 ? F : H;
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt) {
+      if (n == 0) reduce_tile(acc0[jt], dst + off, F, jt * 32, 0, F);
+      else
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) reduce_tile(accH[n > 0 ? n - 1 : 0][jt][ct], dst + off, H, jt * 32, ct * 32, H);
+    }
+    off += (size_t)H * din;
+    // bias: lane (i, hf) holds its half's sum for column jt*32 + i; 8 partial sums per column
+    __syncthreads();
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt) G[(jt * 4 + wave) * 64 + l] = bacc[n][jt];
+    __syncthreads();
+    if (threadIdx.x < H) {
+      const int jt = threadIdx.x >> 5, c = threadIdx.x & 31;
+      float s = 0.0f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) s += G[(jt * 4 + w) * 64 + c] + G[(jt * 4 + w) * 64 + 32 + c];
+      dst[off + threadIdx.x] = s;
+    }
     off += H;
   }
 }
@@ -723,9 +900,15 @@ int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_r
   const dim3 g2(nw);
   const int h_ = d->hidden, nh_ = d->n_hidden;
 #define RAD_SMALL(HH, NN) hipLaunchKernelGGL((radial_bwd_small_kernel<HH, NN>), g2, dim3(256), 0, st, grad_h, n_edges, *d, zsave, feats, part_h)
-  if (h_ == 64) { if (nh_ == 1) RAD_SMALL(64, 1); else if (nh_ == 2) RAD_SMALL(64, 2); else RAD_SMALL(64, 3); }
-  else { if (nh_ == 1) RAD_SMALL(32, 1); else if (nh_ == 2) RAD_SMALL(32, 2); else RAD_SMALL(32, 3); }
+#define RAD_SMALL2(HH, NN) hipLaunchKernelGGL((radial_bwd_small2_kernel<HH, NN>), g2, dim3(256), 0, st, grad_h, n_edges, *d, zsave, feats, part_h)
+  if (h_ == 64) {
+    if (nh_ == 1) RAD_SMALL2(64, 1);
+    else if (nh_ == 2) { if (RAD_S2_H64N2) RAD_SMALL2(64, 2); else RAD_SMALL(64, 2); }
+    else RAD_SMALL(64, 3);
+  }
+  else { if (nh_ == 1) RAD_SMALL2(32, 1); else if (nh_ == 2) RAD_SMALL2(32, 2); else RAD_SMALL2(32, 3); }
 #undef RAD_SMALL
+#undef RAD_SMALL2
   if (int rc = eelg_check_launch("radial_bwd_small")) return rc;
   const dim3 g3((W + 127) / 128, ns);
   RAD_LAUNCH3(radial_bwd_wo_kernel, g3, grad_w, n_edges, W, zsave, tps, part_wo);
