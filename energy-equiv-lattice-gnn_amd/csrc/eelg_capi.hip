@@ -464,6 +464,10 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
+  // LDS-DMA pieces of 16 B, as the fp32 kernel (bf16 weight rows are wn * 2 B, a multiple of 16)
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(sh) |
+        reinterpret_cast<uintptr_t>(w)) & 15) != 0)
+    return fail(-2, "tp_fwd_bf16: x, sh and w must be 16-byte aligned");
   hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(64 * c->fwpb), 0, (hipStream_t)stream,
                      x, sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
                      agg);
@@ -591,8 +595,13 @@ int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* s
                  void* stream) {
   if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(cgc_fwd_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                     pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
+  if (D > 128) return fail(-2, "cgc_fwd: D = %d > 128 not built", D);
+  if (D > 64)
+    hipLaunchKernelGGL(cgc_fwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
+  else
+    hipLaunchKernelGGL(cgc_fwd_kernel<1>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
   return check_launch("cgc_fwd");
 }
 

@@ -16,30 +16,56 @@
 __device__ __forceinline__ float cgc_softplus(float z) { return z > 20.0f ? z : log1pf(expf(z)); }
 __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + expf(-z)); }
 
+// Forward: a receiver's in-edges are taken CGC_EB at a time: their sender indices are
+// wave-uniform (one scalar load batch), and every lane issues the batch's gathers of Ps[s] and
+// Ep[e] before it evaluates any of them, so a receiver costs about three memory round trips
+// instead of two per edge.  A lane owns channels lane + 64 k, k < CPL (CPL = ceil(D / 64)).
+#define CGC_EB 4
+template <int CPL>
 __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
     const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, float* __restrict__ agg) {
-  const int node = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (node >= n_nodes) return;
   const int beg = rowptr[node], end = rowptr[node + 1];
   const int D2 = 2 * D;
   const float sc = row_scale ? row_scale[node] : 1.0f;
   const float* __restrict__ prn = pr + (size_t)node * D2;
-  for (int c = lane; c < D; c += 64) {
-    const float rv = prn[c], rm = prn[D + c];
-    float acc = 0.0f;
-    int s_next = beg < end ? sender[beg] : 0;
-    for (int e = beg; e < end; ++e) {
-      const int s = s_next;
-      if (e + 1 < end) s_next = sender[e + 1];
-      const float zv = ps[(size_t)s * D2 + c] + rv + ep[(size_t)e * D2 + c];
-      const float zm = ps[(size_t)s * D2 + D + c] + rm + ep[(size_t)e * D2 + D + c];
-      acc += cgc_softplus(zv) * cgc_sigmoid(zm);
-    }
-    agg[(size_t)node * D + c] = acc * sc;
+  float rv[CPL], rm[CPL], acc[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = min(lane + 64 * k, D - 1);
+    rv[k] = prn[c];
+    rm[k] = prn[D + c];
+    acc[k] = 0.0f;
   }
+  for (int e0 = beg; e0 < end; e0 += CGC_EB) {
+    int s[CGC_EB];
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j) s[j] = sender[min(e0 + j, end - 1)];
+    float zv[CGC_EB][CPL], zm[CGC_EB][CPL];
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j) {
+      const int e = min(e0 + j, end - 1);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = min(lane + 64 * k, D - 1);
+        zv[j][k] = ps[(size_t)s[j] * D2 + c] + ep[(size_t)e * D2 + c];
+        zm[j][k] = ps[(size_t)s[j] * D2 + D + c] + ep[(size_t)e * D2 + D + c];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j)
+      if (e0 + j < end)   // uniform
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+          acc[k] += cgc_softplus(zv[j][k] + rv[k]) * cgc_sigmoid(zm[j][k] + rm[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+    if (lane + 64 * k < D) agg[(size_t)node * D + lane + 64 * k] = acc[k] * sc;
 }
 
 // Backward: per receiver, recompute z_e and write dz_e = d msg / d z_e (.) g_n for every

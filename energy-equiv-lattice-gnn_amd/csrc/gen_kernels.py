@@ -41,8 +41,8 @@ TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 # in the step 0.438 vs 0.446 ms)
 TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
 # tp_fwd: the rows of the next two edges (x / SH / weight) prefetched into LDS by LDS-DMA
-# (global_load_lds) instead of a second register set (fp32 storage only); 0 = the register
-# pipeline (the bf16-storage kernel's form).  One edge in flight by LDS-DMA measured slower
+# (global_load_lds) instead of a second register set, for fp32 and bf16 weight storage; 0 = the
+# register pipeline.  One edge in flight by LDS-DMA measured slower
 # (r03ag/r03ai: 0.499 vs 0.486 ms kbench) and was removed.
 TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
 # LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
@@ -282,9 +282,10 @@ def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
     return out
 
 
-def _glds_chunks(groups, nshp, node_off):
+def _glds_chunks(groups, nshp, node_off, wes: int = 4):
     """Per path group: the 16-B chunk list of one half-wave's rows for one edge (x blocks of
-    x[sender], the SH row, the group's weight slices) and the image float offsets."""
+    x[sender], the SH row, the group's weight slices of ``wes`` bytes per weight) and the image
+    offsets in 4-byte units."""
     glist = []
     for grp in groups:
         need_l1 = sorted({p.l1 for p in grp})
@@ -297,7 +298,7 @@ def _glds_chunks(groups, nshp, node_off):
         chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
         for p in grp:
             fo_w[p.slot] = 4 * len(chunks)
-            chunks += [(2, 4 * p.slot * MUL + 16 * cc) for cc in range(8)]
+            chunks += [(2, wes * p.slot * MUL + 16 * cc) for cc in range(wes * MUL // 16)]
         glist.append((need_l1, need_l2, chunks, fo_x, fo_sh, fo_w))
     return glist
 
@@ -351,7 +352,7 @@ def _glds_compute(grp, cur, accs) -> List[str]:
     return L
 
 
-def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]:
+def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = False) -> List[str]:
     """tp_fwd with the rows of edges e+1 AND e+2 in flight by LDS-DMA (two LDS images per
     half-wave) while edge e computes.  The per-half-wave stream state (edge, receiver, the
     rowptr entries, the sender indices) is wave-uniform per half and kept in SGPRs with scalar
@@ -362,13 +363,14 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]
     WPB = TP_FWD_WPB
     TN = 2 * WPB * TP_NPH
     ng = len(groups)
-    glist = _glds_chunks(groups, nshp, node_off)
+    glist = _glds_chunks(groups, nshp, node_off, 2 if bf else 4)
     NJ = max(-(-len(g[2]) // 64) for g in glist)
     NI = NJ * 64
     L: List[str] = []
     wpe = f" __attribute__((amdgpu_waves_per_eu({TP_FWD_WPE})))" if TP_FWD_WPE else ""
-    L.append(f"__global__ __launch_bounds__({64 * WPB}){wpe} void tp_fwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    WT = "unsigned short" if bf else "float"
+    L.append(f"__global__ __launch_bounds__({64 * WPB}){wpe} void tp_fwd_{name}{'_bw' if bf else ''}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
     L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
@@ -458,11 +460,21 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off) -> List[str]
             L.append(f"      asm volatile(\"ds_read_b128 %0, %1 offset:{4 * fo_sh + 16 * blk}\" : \"=v\"(ty{blk}) : \"v\"(imb));")
             live.append(f"ty{blk}")
             after.append(" ".join(f"y{j} = ty{blk}[{j - 4 * blk}];" for j in need_y if j // 4 == blk))
-        L.append("      { const unsigned wa = imb + 4 * u;")
-        for p in grp:
-            L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(w{p.slot}) : \"v\"(wa));")
-            live.append(f"w{p.slot}")
-        L.append("      }")
+        if bf:
+            # bf16 weights: ds_read_u16, widened exactly after the wait
+            L.append("      unsigned " + ", ".join(f"wr{p.slot}" for p in grp) + ";")
+            L.append("      { const unsigned wa = imb + 2 * u;")
+            for p in grp:
+                L.append(f"        asm volatile(\"ds_read_u16 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(wr{p.slot}) : \"v\"(wa));")
+                live.append(f"wr{p.slot}")
+                after.append(f"w{p.slot} = __uint_as_float(wr{p.slot} << 16);")
+            L.append("      }")
+        else:
+            L.append("      { const unsigned wa = imb + 4 * u;")
+            for p in grp:
+                L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(w{p.slot}) : \"v\"(wa));")
+                live.append(f"w{p.slot}")
+            L.append("      }")
         for k in range(0, len(live), 24):
             ops = ", ".join(f'"+v"({v})' for v in live[k: k + 24])
             L.append(f'      asm volatile("s_waitcnt lgkmcnt(0)" : {ops} : : "memory");')
@@ -528,8 +540,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
-    if TP_FWD_GLDS == 2 and not bf:
-        L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off)
+    if TP_FWD_GLDS == 2:
+        L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf)
     else:
         L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
         L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")

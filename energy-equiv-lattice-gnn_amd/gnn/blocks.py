@@ -210,12 +210,14 @@ class TensorProductInteractionBlock(torch.nn.Module):
             self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
         self.conv_tp = TensorProduct(self._node_feats_irreps, self.edge_attrs_irreps, irreps_mid,
                                      instructions)
-        # the fused radial-MLP kernels (csrc/eelg_radial.hip) are built for these shapes
+        # the fused radial-MLP kernels (csrc/eelg_radial.hip) are built for inter_MLP_dim 32 / 64,
+        # inter_MLP_layers 2..4 and <= 32 edge features (the reference default: 12 -> 64 -> 64);
+        # other shapes run the same torch.nn.Sequential on the device (library GEMMs + SiLU), the
+        # reference's own formulation of conv_tp_weights
         n_feat = self.edge_feats_irreps.num_irreps
-        if MLP_dim not in (32, 64) or not 2 <= MLP_layers <= 4 or not 1 <= n_feat <= 32:
-            raise ValueError(f"radial MLP {n_feat}->{MLP_dim}x{MLP_layers - 1}: the HIP kernels are "
-                             "built for inter_MLP_dim 32 or 64, inter_MLP_layers 2..4 and <= 32 "
-                             "edge features")
+        if MLP_layers < 2:
+            raise ValueError(f"inter_MLP_layers {MLP_layers}: the radial MLP needs at least one hidden layer")
+        self._radial_hip = MLP_dim in (32, 64) and MLP_layers <= 4 and 1 <= n_feat <= 32
         layer = torch.nn.Linear(MLP_dim, self.conv_tp.weight_numel, bias=False)
         torch.nn.init.xavier_uniform_(layer.weight, gain=10)
         self.conv_tp_weights = torch.nn.Sequential(
@@ -246,7 +248,10 @@ class TensorProductInteractionBlock(torch.nn.Module):
 
     def radial_weights(self, edge_feats: torch.Tensor) -> torch.Tensor:
         """``conv_tp_weights(edge_feats)`` (``gnn/blocks.py:590``): the per-edge TP weights."""
-        return ops.radial_mlp(edge_feats, self.conv_tp_weights, self.storage_dtype)
+        if self._radial_hip:
+            return ops.radial_mlp(edge_feats, self.conv_tp_weights, self.storage_dtype)
+        ops._require_device(edge_feats)
+        return self.conv_tp_weights(edge_feats).to(self.storage_dtype)
 
     def forward(self, node_feats, edge_attrs, edge_feats, edge_index: EdgeIndex,
                 node_attrs: Optional[torch.Tensor] = None,

@@ -315,7 +315,12 @@ class _TPInteraction(torch.autograd.Function):
     def forward(ctx, x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
         # w: fp32, or bf16 storage (BASELINE config 5; fp32 arithmetic in the kernels)
         bf = w.dtype == torch.bfloat16
-        x, w = _a16(x), (w.contiguous() if bf else _a16(w))
+        x = _a16(x)
+        if bf:
+            w = w.contiguous()
+            w = w if w.data_ptr() % 16 == 0 else w.clone()
+        else:
+            w = _a16(w)
         if sh.dtype != torch.float32:
             raise TypeError(f"expected float32 SH, got {sh.dtype}")
         sh = padded_sh(sh)

@@ -70,7 +70,8 @@ int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const 
 /* BASELINE config 5 (bf16 storage, fp32 arithmetic): eelg_tp_fwd / eelg_tp_bwd with the
  * edge-sized tensors w, grad_w [E, weight_numel] and gxe [E, din] held as bf16 bit patterns
  * (uint16, round-to-nearest-even on store).  Same reference call sites
- * (gnn/blocks.py:590-597). */
+ * (gnn/blocks.py:590-597).  eelg_tp_fwd_bf16 moves rows by LDS-DMA like eelg_tp_fwd: x, sh
+ * and w must be 16-byte aligned; -2 otherwise. */
 int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
                      const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream);
 int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, const int* sender,
@@ -168,7 +169,8 @@ int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, 
  *                                            cgc_vanilla.py:20-25, gnn/blocks.py:960-966)
  * with the linear split by input block: ps = x W_s^T, pr = x W_r^T + b ([N, 2D], values
  * then multipliers), ep = edge_ft W_e^T ([E, 2D], receiver-sorted edge order).
- * agg[n] = row_scale[n] * sum_e softplus(zv) sigmoid(zm)  (row_scale NULL -> 'sum'). */
+ * agg[n] = row_scale[n] * sum_e softplus(zv) sigmoid(zm)  (row_scale NULL -> 'sum').
+ * Built for D <= 128 (the benchmark models use 128 and 64); -2 otherwise. */
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
                  void* stream);

@@ -584,3 +584,32 @@ def test_linear_packed_split_path_is_fp32_accurate(irreps_in, irreps_out):
     record_parity(f"linear_x6_{o.irreps_in.dim}", x6=errs[True], f32=errs[False])
     for a, b in zip(errs[True], errs[False]):
         assert a <= 1.5 * b + 1e-7, errs
+
+
+@pytest.mark.parametrize("mlp_dim,mlp_layers", [(16, 3), (48, 2), (64, 5)])
+def test_model_with_other_radial_mlp_shapes_matches_oracle(mlp_dim, mlp_layers):
+    """``inter_MLP_dim`` / ``inter_MLP_layers`` outside the fused radial kernels' set run the
+    reference's Sequential on the device (``TensorProductInteractionBlock._radial_hip`` False);
+    the rest of the path is the HIP one.  Same tolerances as the model test above."""
+    from gnn.model import EnergyEquivGNN
+    from gnn.train import stiffness_loss
+    b, bd, csr, rmax = _setup()
+    p = params(2, max_edge_radius=rmax, inter_MLP_dim=mlp_dim, inter_MLP_layers=mlp_layers)
+    torch.manual_seed(0)
+    o = omodel.EnergyEquivGNN(p).double()
+    m = EnergyEquivGNN(p).to(DEV)
+    assert not any(lay.interaction._radial_hip for lay in m.stiffness_head.layers)
+    copy_params(o, m)
+    bo = batch_to(b, "cpu", torch.float64)
+    co = o(bo)["stiffness"]
+    lo = oracle_loss(co, bo.stiffness)
+    lo.backward()
+    cm = m(bd)["stiffness"]
+    lm = stiffness_loss(cm, bd.stiffness)
+    lm.backward()
+    po = dict(o.named_parameters())
+    worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
+    record_parity(f"model_mlp{mlp_dim}x{mlp_layers}", stiffness=rel_err(cm, co), grad_params=worst)
+    assert rel_err(cm, co) < 1e-4
+    assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
+    assert worst < 1e-5

@@ -199,10 +199,10 @@ def test_product_model_param_names_match_oracle():
     assert sum(v.numel() for v in m.parameters()) == 223186
 
 
-def test_radial_mlp_is_hip_only_and_checks_shapes():
-    """The radial MLP runs only as the fused HIP kernels (tests/test_gpu_radial.py holds
-    their parity tests): a CPU input raises, and shapes the kernels are not built for fail
-    at construction, naming the supported set."""
+def test_radial_mlp_is_device_only_and_checks_shapes():
+    """The radial MLP runs on the device only: the fused HIP kernels for their shapes
+    (tests/test_gpu_radial.py holds their parity tests), the reference's Sequential on the
+    device for other inter_MLP_dim / inter_MLP_layers; a CPU input raises either way."""
     from gnn import ops
     from gnn.blocks import TensorProductInteractionBlock
     mlp = torch.nn.Sequential(torch.nn.Linear(12, 64), torch.nn.SiLU(),
@@ -211,11 +211,16 @@ def test_radial_mlp_is_hip_only_and_checks_shapes():
         ops.radial_mlp(torch.randn(5, 12), mlp)
     hid = "32x0e+32x1o+32x2e+32x3o+32x4e"
     sh = "1x0e+1x1o+1x2e+1x3o+1x4e"
-    for dim, layers in ((48, 3), (64, 5), (128, 3)):
-        with pytest.raises(ValueError, match="inter_MLP_dim 32 or 64"):
-            TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=dim,
-                                          MLP_layers=layers)
-    TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=32, MLP_layers=4)
+    # shapes outside the fused kernels' set run the reference's Sequential on the device; a CPU
+    # tensor still raises
+    for dim, layers in ((48, 3), (64, 5), (128, 3), (16, 2)):
+        blk = TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=dim, MLP_layers=layers)
+        assert not blk._radial_hip
+        with pytest.raises(RuntimeError, match="HIP device"):
+            blk.radial_weights(torch.randn(5, 12))
+    assert TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=32, MLP_layers=4)._radial_hip
+    with pytest.raises(ValueError, match="at least one hidden layer"):
+        TensorProductInteractionBlock(hid, sh, "12x0e", hid, 4.0, MLP_dim=32, MLP_layers=1)
 
 
 def test_wgrad_split_k_matches_matmul():
