@@ -15,6 +15,8 @@ typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned sho
                                   unsigned short*, const int*);
 // sender-order backward: (x, sh, w, sperm, srowptr, receiver, n_nodes, grad_agg, inv_norm,
 // grad_w, grad_x)
+typedef void (*eelg_tp_bwr_fn)(const float*, const float*, const float*, const int*, const int*, int,
+                               const float*, float, float*, float*);
 typedef void (*eelg_tp_bws_fn)(const float*, const float*, const float*, const int*, const int*,
                                const int*, int, const float*, float, float*, float*);
 typedef void (*eelg_tp_bws_bf_fn)(const float*, const float*, const unsigned short*, const int*,
@@ -39,6 +41,7 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_bf_fn bwd_bf;
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
+  eelg_tp_bwr_fn bwr;        // receiver-major streaming backward (fp32)
 };
 
 struct eelg_sc_cfg {

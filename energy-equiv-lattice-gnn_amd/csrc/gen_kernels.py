@@ -505,6 +505,191 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     return L
 
 
+def _emit_tp_bwd_rmaj(name, bgroups, din, nshp, dmid, wn, node_off) -> List[str]:
+    """tp_bwd in receiver-major streaming form ("tp_bwr"): the mapping, grid and LDS-DMA edge
+    pipeline of the forward (_emit_tp_fwd_glds2: a half-wave owns TP_NPH consecutive receivers
+    and streams their in-edges, the x / SH / weight rows of edges e+1 and e+2 in flight by
+    LDS-DMA), over the backward's l1 groups (each owns a disjoint slice of gxe).  A receiver's
+    grad_agg slices are loaded into registers once, when its first in-edge comes up, instead of
+    once per in-edge; per edge the lanes write grad_w of the group's paths and the group's gxe
+    slice (exec-masked to the half-waves that still have edges).  Same arithmetic as tp_bwd
+    (bitwise-equal results)."""
+    WPB = TP_FWD_WPB
+    TN = 2 * WPB * TP_NPH
+    ng = len(bgroups)
+    glist = _glds_chunks(bgroups, nshp, node_off, 4)
+    NJ = max(-(-len(g[2]) // 64) for g in glist)
+    NI = NJ * 64
+    L: List[str] = []
+    L.append(f"__global__ __launch_bounds__({64 * WPB}) void tp_bwr_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    const float* __restrict__ gagg, float inv_norm, float* __restrict__ gw,")
+    L.append("    float* __restrict__ gxe) {")
+    L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
+    L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5;")
+    L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
+    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
+    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
+    L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
+    L.append("  if (nw0 >= n_nodes) return;   // uniform per wave")
+    L.append("  float4* __restrict__ ib = &img_[wv][0][0][0];")
+    L.append("  const char* pad_ = reinterpret_cast<const char*>(eelg_tp_pad);")
+    L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)ib);")
+    for h in (0, 1):
+        L.append(f"  const int n0_{h} = min(nw0 + {h * TP_NPH}, n_nodes), n1_{h} = min(n0_{h} + {TP_NPH}, n_nodes);")
+        L.append(f"  int e_{h} = rowptr[n0_{h}];")
+        L.append(f"  const int eend_{h} = rowptr[n1_{h}];")
+        L.append(f"  int node_{h} = n0_{h}, nend_{h} = rowptr[min(n0_{h} + 1, n1_{h})], "
+                 f"nend2_{h} = rowptr[min(n0_{h} + 2, n1_{h})], gn_{h} = -1;")
+    L.append("  switch (grp) {")
+    for gi, grp in enumerate(bgroups):
+        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
+        assert len(need_l1) == 1
+        l1 = need_l1[0]
+        d1 = 2 * l1 + 1
+        nj = -(-len(chunks) // 64)
+        L.append(f"  case {gi}: {{ // input block l1 = {l1}: {len(chunks)} chunks of 16 B per half-wave and edge")
+        L += _glds_desc(chunks, nj)
+
+        def issue(buf, ahead):
+            out = ["    {"]
+            for h in (0, 1):
+                out.append(f"      {{ const bool ok_ = e_{h} + {ahead} < eend_{h};")
+                out.append(f"        const int ee_ = ok_ ? e_{h} + {ahead} : 0;")
+                out.append(f"        const int ss_ = ok_ ? sender[ee_] : 0;")
+                out.append(f"        const char* xb = ok_ ? reinterpret_cast<const char*>(x + (size_t)ss_ * {din}) : pad_;")
+                out.append(f"        const char* shb = ok_ ? reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp}) : pad_;")
+                out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")
+                out.append(f"        float4* dst = ib + ({buf}) * {2 * NI} + {h * NI};")
+                for j in range(nj):
+                    out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
+                               f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
+                               f"(__attribute__((address_space(3))) void*)(dst + {64 * j}), 16, 0, 0);")
+                out.append("      }")
+            out.append("    }")
+            return out
+        gregs = [f"g{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
+        L.append("    float " + ", ".join(f"{g} = 0.0f" for g in gregs) + ";")
+        # vector stores per edge: one per path (grad_w) + the gxe slice's vector stores
+        nst = len(grp) + len(vec_store([f"gx{i}" for i in range(d1)], "o", "0"))
+        L += issue("0", 0)
+        L += issue("1", 1)
+        L.append("    int b = 0, it_ = 0;")
+        L.append("    for (;;) {")
+        # edge e's rows landed.  Vector memory operations complete in issue order on gfx9, and in
+        # the steady state edge e's LDS-DMA is followed by the stores of edge e-2, edge e+1's
+        # LDS-DMA and the stores of edge e-1; the first two edges wait for fewer (the counts must
+        # never exceed what is in flight behind the awaited DMA)
+        L.append(f'      if (it_ >= 2) asm volatile("s_waitcnt vmcnt({2 * nj + 2 * nst})" ::: "memory");')
+        L.append(f'      else if (it_ == 1) asm volatile("s_waitcnt vmcnt({2 * nj})" ::: "memory");')
+        L.append('      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        L.append("      ++it_;")
+        L.append(f"      const unsigned imb = lds0 + b * {2 * NI * 16} + hf * {NI * 16};")
+        cur = ([f"x{l1}_{i}" for i in range(d1)]
+               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
+               + [f"w{p.slot}" for p in grp])
+        L.append("      float " + ", ".join(cur) + ";")
+        tdecl = [f"tx{l1}_{i}" for i in range(0, 2 * l1, 2)]
+        if tdecl:
+            L.append("      eelg_f2r " + ", ".join(tdecl) + ";")
+        need_y = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
+        L.append("      eelg_f4r " + ", ".join(f"ty{blk}" for blk in sorted({j // 4 for j in need_y})) + ";")
+        live, after = [], []
+        L.append(f"      {{ const unsigned xa = imb + 4 * ({fo_x[l1]} + u * {d1});")
+        i = 0
+        while i < d1:
+            if i + 1 < d1:
+                L.append(f"        asm volatile(\"ds_read2_b32 %0, %1 offset0:{i} offset1:{i + 1}\" : \"=v\"(tx{l1}_{i}) : \"v\"(xa));")
+                live.append(f"tx{l1}_{i}")
+                after.append(f"x{l1}_{i} = tx{l1}_{i}[0]; x{l1}_{i + 1} = tx{l1}_{i}[1];")
+                i += 2
+            else:
+                L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * i}\" : \"=v\"(x{l1}_{i}) : \"v\"(xa));")
+                live.append(f"x{l1}_{i}")
+                i += 1
+        L.append("      }")
+        for blk in sorted({j // 4 for j in need_y}):
+            L.append(f"      asm volatile(\"ds_read_b128 %0, %1 offset:{4 * fo_sh + 16 * blk}\" : \"=v\"(ty{blk}) : \"v\"(imb));")
+            live.append(f"ty{blk}")
+            after.append(" ".join(f"y{j} = ty{blk}[{j - 4 * blk}];" for j in need_y if j // 4 == blk))
+        L.append("      { const unsigned wa = imb + 4 * u;")
+        for p in grp:
+            L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(w{p.slot}) : \"v\"(wa));")
+            live.append(f"w{p.slot}")
+        L.append("      }")
+        for k in range(0, len(live), 24):
+            ops = ", ".join(f'"+v"({v})' for v in live[k: k + 24])
+            L.append(f'      asm volatile("s_waitcnt lgkmcnt(0)" : {ops} : : "memory");')
+        L += ["      " + a_ for a_ in after]
+        L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
+        # receivers whose in-edges are done (and receivers with none) are skipped
+        for h in (0, 1):
+            L.append(f"      while (node_{h} < n1_{h} && nend_{h} == e_{h}) {{   // uniform")
+            L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
+            L.append("      }")
+        L.append("      if (e_0 >= eend_0 && e_1 >= eend_1) break;")
+        # the current receiver's grad_agg slices, when it changed (lanes of that half only)
+        L.append("      { const bool c0_ = e_0 < eend_0 && node_0 != gn_0, c1_ = e_1 < eend_1 && node_1 != gn_1;")
+        L.append("        if (c0_ || c1_) {   // uniform")
+        L.append("          if (hf ? c1_ : c0_) {")
+        L.append(f"            const float* __restrict__ ge = gagg + (size_t)(hf ? node_1 : node_0) * {dmid};")
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            L += ["            " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
+                                                        f"{p.out_off} + u * {d3}")]
+        L.append("          }")
+        L.append("          if (c0_) gn_0 = node_0;")
+        L.append("          if (c1_) gn_1 = node_1;")
+        L.append("        }")
+        L.append("      }")
+        L += ["  " + ln for ln in issue("b", 2)]
+        # edge e of this lane's half: grad_w of the group's paths and the gxe slice
+        L.append("      const int em_ = hf ? e_1 : e_0;")
+        L.append("      const bool st_ = em_ < (hf ? eend_1 : eend_0);")
+        L.append(f"      float* __restrict__ gwe = gw + (size_t)em_ * {wn} + u;")
+        for i in range(d1):
+            L.append(f"      float gx{i} = 0.0f;")
+        base_pin = cur + [f"gx{i}" for i in range(d1)] + gregs
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
+            byik: Dict[Tuple[int, int], List[str]] = {}
+            for (i, j, k), c in _path_cg(p):
+                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
+            for (i, k), ts in byik.items():
+                L.append(f"        const float m{i}_{k} = {' + '.join(ts)};")
+            gterms = []
+            for k in range(d3):
+                ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
+                if ts:
+                    gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
+            gexpr = " + ".join(gterms) if gterms else "0.0f"
+            L.append(f"        if (st_) gwe[{p.slot * MUL}] = cp * ({gexpr});")
+            L.append(f"        const float hw = cp * w{p.slot};")
+            for i in range(d1):
+                ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
+                if ts:
+                    L.append(f"        gx{i} = fmaf(hw, {' + '.join(ts)}, gx{i});")
+            L.append("      }")
+            L.append("      " + pin(base_pin))
+        L.append("      if (st_) {")
+        L.append(f"        float* __restrict__ o = gxe + (size_t)em_ * {din};")
+        L += ["        " + ln for ln in vec_store([f"gx{i}" for i in range(d1)], "o", f"{node_off[l1]} + u * {d1}")]
+        L.append("      }")
+        L.append("      ++e_0; ++e_1; b ^= 1;")
+        L.append("    }")
+        L.append('    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the wave')
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -776,6 +961,9 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  default: break;")
     L.append("  }")
     L.append("}")
+
+    if not bf:
+        L += _emit_tp_bwd_rmaj(name, bgroups, din, nshp, dmid, wn, node_off)
 
     # ---------------- backward in sender order ----------------
     # One half-wave owns one SENDER node and walks its out-edges through the sender CSR
@@ -1568,7 +1756,7 @@ def main(outdir: str) -> None:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                      f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
+                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw, tp_bwr_{name}}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:

@@ -58,6 +58,7 @@ _SIGS = {
     "eelg_linear_pack_size": ([_P], ctypes.c_longlong),
     "eelg_linear_pack": ([_P, _P, _P, _P], _I),
     "eelg_linear_fwd_pk": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
+    "eelg_tp_bwd_csr": ([_I, _P, _P, _P, _P, _P, _I, _P, ctypes.c_float, _P, _P, _P], _I),
     "eelg_split_bf16x3": ([_P, ctypes.c_longlong, _P, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
@@ -124,7 +125,11 @@ def load() -> ctypes.CDLL:
             "(there is no CPU fallback for the HIP hot path)")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (args, res) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if os.environ.get("EELG_LIB"):   # an older variant build (experiments): entry absent
+                continue
+            raise EELGError(f"{LIB_PATH} lacks {name}: stale build, rebuild the library")
         fn.argtypes = args
         fn.restype = res
     _lib = lib

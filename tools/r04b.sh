@@ -1,31 +1,34 @@
 #!/bin/bash
-# SC coefficient stream by LDS-DMA: parity of the new kernels (default + variants), kbench A/B
-# against the round-3 SMEM stream (variants/head), then the full GPU suite + bench + profiles
-set -e -o pipefail
+# Round-4 first GPU pass over the new kernels (SC coefficient stream by LDS-DMA, split-bf16 radial
+# and linears, receiver-major tp_bwd, bf16 LDS-DMA tp_fwd, batched CGC): parity of each, then
+# kbench A/B against the round-3 build (variants/head).  A failing test (pytest rc 1) does not
+# stop the script; any other failure (fault, abort, timeout) does.
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/r04b; mkdir -p "$O"
 cd "$R"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 400 --timeout-method thread \
-   -k "symcon or model_forward_backward_matches_oracle" > "$O/t_main.log" 2>&1 || { tail -30 "$O/t_main.log"; exit 3; }
-echo "main: $(tail -1 $O/t_main.log)"
-for v in csb16d4 csb16d2 csc256 csb32d3; do
-  EELG_LIB=$R/variants/libeelg_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread \
-     -k "symcon" > "$O/t_$v.log" 2>&1 || { tail -30 "$O/t_$v.log"; exit 3; }
-  echo "$v: $(tail -1 $O/t_$v.log)"
-done
-timeout -k 10 300 python -u -m pytest tests/test_gpu_radial.py -x -q --timeout 240 --timeout-method thread > "$O/t_radial.log" 2>&1 || { tail -30 "$O/t_radial.log"; exit 3; }
-EELG_LIB=$R/variants/libeelg_rads2.so timeout -k 10 300 python -u -m pytest tests/test_gpu_radial.py -x -q --timeout 240 --timeout-method thread > "$O/t_radial_s2.log" 2>&1 || { tail -30 "$O/t_radial_s2.log"; exit 3; }
-echo "radial s2: $(tail -1 $O/t_radial_s2.log)"
-echo "radial: $(tail -1 $O/t_radial.log)"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "linear" > "$O/t_lin.log" 2>&1 || { tail -30 "$O/t_lin.log"; exit 3; }
-echo "linear: $(tail -1 $O/t_lin.log)"
+step() {   # step <log> <timeout> <cmd...>: rc 0 / 1 continue, anything else ends the script
+  local log=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?
+  echo "[$log] rc=$rc $(tail -1 "$O/$log")"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; tail -20 "$O/$log"; exit $rc; fi
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+step t_symcon.log 400 $PYT tests/test_gpu_parity.py -k "symcon"
+step t_radial.log 300 $PYT tests/test_gpu_radial.py
+step t_lin.log 300 $PYT tests/test_gpu_parity.py -k "linear"
+step t_tpbwr.log 300 $PYT tests/test_gpu_fullsize.py -k "receiver_major or edgeless or no_edges"
+step t_model.log 600 $PYT tests/test_gpu_parity.py -k "model_forward_backward_matches_oracle or other_radial"
+step t_bf16.log 400 $PYT tests/test_gpu_bf16.py
+step t_cgc.log 400 $PYT tests/test_cgc.py -m gpu
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 python3 "$R/variants/head/tools/kbench.py" --reps 20 --only "sc_|radial|lin" > "$O/k_head.txt" 2>&1
-echo "== head"; grep " ms" "$O/k_head.txt" | cut -c1-90
-bash "$R/tools/ab_kbench.sh" "sc_|radial|lin" main
-EELG_LIN_X6=0 timeout -k 10 200 python3 "$R/tools/kbench.py" --reps 20 --only "lin" > "$O/k_main_linf32.txt" 2>&1
-echo "== main, EELG_LIN_X6=0"; grep " ms" "$O/k_main_linf32.txt" | cut -c1-90
-bash "$R/tools/ab_kbench.sh" "radial" rads2
-bash "$R/tools/ab_kbench.sh" "sc_" csb16d4 csb16d2 csc256 csb32d3
-cd "$R"
+step k_head.txt 200 python3 "$R/variants/head/tools/kbench.py" --reps 20
+grep " ms" "$O/k_head.txt" | cut -c1-100
+step k_main.txt 200 python3 "$R/tools/kbench.py" --reps 20
+grep " ms" "$O/k_main.txt" | cut -c1-100
+step k_linf32.txt 200 env EELG_LIN_X6=0 python3 "$R/tools/kbench.py" --reps 20 --only "lin"
+grep " ms" "$O/k_linf32.txt" | cut -c1-100
+for v in csb16d4 csb16d2 csc256 csb32d3 rads2; do
+  step k_$v.txt 200 env EELG_LIB=$R/variants/libeelg_$v.so python3 "$R/tools/kbench.py" --reps 20 --only "sc_|radial"
+  grep " ms" "$O/k_$v.txt" | cut -c1-100
+done
 echo done > "$O/ok"
