@@ -112,6 +112,21 @@ __device__ __forceinline__ void eelg_split8(const float* v, uint4* p) {
     EELG_MFMA_BF(acc, (a)[2], (b)[0]); EELG_MFMA_BF(acc, (a)[0], (b)[1]);       \
     EELG_MFMA_BF(acc, (a)[1], (b)[0]); EELG_MFMA_BF(acc, (a)[0], (b)[0]);       \
   } while (0)
+// the same with the five small products in their own accumulator (lo) and only a0 b0 in hi:
+// over a long K the hi chain rounds once per K block instead of six times, and lo (<= 2^-7 of
+// hi) adds nothing visible; the caller returns hi + lo.  For K in the thousands (radial grad_h,
+// K = the radial outputs) this is more accurate than an fp32 MFMA chain.
+#define EELG_X6HL(hi, lo, a, b)                                                   \
+  do {                                                                          \
+    EELG_MFMA_BF(lo, (a)[0], (b)[2]); EELG_MFMA_BF(lo, (a)[1], (b)[1]);         \
+    EELG_MFMA_BF(lo, (a)[2], (b)[0]); EELG_MFMA_BF(lo, (a)[0], (b)[1]);         \
+    EELG_MFMA_BF(lo, (a)[1], (b)[0]); EELG_MFMA_BF(hi, (a)[0], (b)[0]);         \
+  } while (0)
+#define EELG_X3HL(hi, lo, a, b)                                                   \
+  do {                                                                          \
+    EELG_MFMA_BF(lo, (a), (b)[2]); EELG_MFMA_BF(lo, (a), (b)[1]);               \
+    EELG_MFMA_BF(hi, (a), (b)[0]);                                              \
+  } while (0)
 // acc += A B with A exactly bf16 (a single part, e.g. bf16 storage) and B split (b[3])
 #define EELG_X3(acc, a, b)                                                        \
   do {                                                                          \

@@ -975,7 +975,8 @@ __global__ __launch_bounds__(256) void lin_pack_kernel(const float* __restrict__
   }
   uint4 p[3];
   eelg_split8(v, p);
-  const size_t o = (size_t)lin_pack_slot_off(desc, s) + ((size_t)(jt * nch + c) * 2 + kb) * 384 + lane;
+  // a K block holds its 3 parts x 64 pieces: the same order lin_fwd_x6 reads
+  const size_t o = (size_t)lin_pack_slot_off(desc, s) + ((size_t)(jt * nch + c) * 2 + kb) * 192 + lane;
 #pragma unroll
   for (int q = 0; q < 3; ++q) pk[o + q * 64] = p[q];
 }

@@ -291,11 +291,11 @@ __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restri
     }
   };
 
-  rad_f32x16 acc[NT];
+  rad_f32x16 acc[NT], lo[NT];   // hi (a0 b0) and lo (the small part products), EELG_X6HL
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[ct][r] = 0.0f;
+    for (int r = 0; r < 16; ++r) acc[ct][r] = lo[ct][r] = 0.0f;
   load_b(0);
   store_b(0);
   load_a(0);
@@ -333,9 +333,9 @@ __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restri
 #pragma unroll
         for (int p = 0; p < 3; ++p) b[p] = bb[((p * NT + ct) * 2 + kb) * 64];
         if (BF)
-          EELG_X3(acc[ct], ap[0], b);
+          EELG_X3HL(acc[ct], lo[ct], ap[0], b);
         else
-          EELG_X6(acc[ct], ap, b);
+          EELG_X6HL(acc[ct], lo[ct], ap, b);
       }
     }
     if (c + 1 < nchunk) store_b((c + 1) & 1);
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void radial_bwd_gh_kernel(const void* __restri
   for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      rad_bst(rh, ((uint32_t)(e0 + rad_row(r, hf)) * H + ct * 32 + i) * 4u, acc[ct][r]);
+      rad_bst(rh, ((uint32_t)(e0 + rad_row(r, hf)) * H + ct * 32 + i) * 4u, acc[ct][r] + lo[ct][r]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -688,11 +688,11 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
   const bool bmine = threadIdx.x < NFR;
   const int bk = threadIdx.x & 31, bh = (threadIdx.x >> 5) & 1, bkb = (threadIdx.x >> 6) & 1,
             bct = threadIdx.x >> 7;
-  rad_f32x16 acc[NT];
+  rad_f32x16 acc[NT], lo[NT];   // hi / lo accumulators (EELG_X6HL): K = a split's edges
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[ct][r] = 0.0f;
+    for (int r = 0; r < 16; ++r) acc[ct][r] = lo[ct][r] = 0.0f;
   float an[16], zn[8];
   auto load = [&](int t) {
     // A[j][e]: e = t*32 + 16 kb + 8 hf + u; rows past E read zeros
@@ -747,9 +747,9 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
 #pragma unroll
         for (int p = 0; p < 3; ++p) b[p] = bb[p * NFR + (ct * 2 + kb) * 64];
         if (BF)
-          EELG_X3(acc[ct], ap[kb][0], b);
+          EELG_X3HL(acc[ct], lo[ct], ap[kb][0], b);
         else
-          EELG_X6(acc[ct], ap[kb], b);
+          EELG_X6HL(acc[ct], lo[ct], ap[kb], b);
       }
   }
   const int jb = blockIdx.x * 128 + wave * 32;
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256) void radial_bwd_wo_kernel(const void* __restri
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = jb + rad_row(r, hf);
-      if (jj < W) part[((size_t)s * W + jj) * H + ct * 32 + i] = acc[ct][r];
+      if (jj < W) part[((size_t)s * W + jj) * H + ct * 32 + i] = acc[ct][r] + lo[ct][r];
     }
 }
 

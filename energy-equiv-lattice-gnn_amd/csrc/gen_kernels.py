@@ -404,7 +404,7 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
                 # a half past its last edge reads the pad row (no edge row need exist: E = 0)
                 out.append(f"      {{ const bool ok_ = e_{h} + {ahead} < eend_{h};")
                 out.append(f"        const int ee_ = ok_ ? e_{h} + {ahead} : 0;")
-                out.append(f"        const int ss_ = ok_ ? sender[ee_] : 0;")
+                out.append(f"        const int ss_ = *(ok_ ? sender + ee_ : reinterpret_cast<const int*>(pad_));   // never a load through a null sender (E = 0)")
                 out.append(f"        const char* xb = ok_ ? reinterpret_cast<const char*>(x + (size_t)ss_ * {din}) : pad_;")
                 out.append(f"        const char* shb = ok_ ? reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp}) : pad_;")
                 out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")
@@ -559,7 +559,7 @@ def _emit_tp_bwd_rmaj(name, bgroups, din, nshp, dmid, wn, node_off) -> List[str]
             for h in (0, 1):
                 out.append(f"      {{ const bool ok_ = e_{h} + {ahead} < eend_{h};")
                 out.append(f"        const int ee_ = ok_ ? e_{h} + {ahead} : 0;")
-                out.append(f"        const int ss_ = ok_ ? sender[ee_] : 0;")
+                out.append(f"        const int ss_ = *(ok_ ? sender + ee_ : reinterpret_cast<const int*>(pad_));   // never a load through a null sender (E = 0)")
                 out.append(f"        const char* xb = ok_ ? reinterpret_cast<const char*>(x + (size_t)ss_ * {din}) : pad_;")
                 out.append(f"        const char* shb = ok_ ? reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp}) : pad_;")
                 out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")

@@ -13,9 +13,8 @@ step() {   # step <log> <timeout> <cmd...>: rc 0 / 1 continue, anything else end
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; tail -20 "$O/$log"; exit $rc; fi
 }
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-step t_symcon.log 400 $PYT tests/test_gpu_parity.py -k "symcon"
-step t_radial.log 300 $PYT tests/test_gpu_radial.py
 step t_lin.log 300 $PYT tests/test_gpu_parity.py -k "linear"
+step t_radial.log 300 $PYT tests/test_gpu_radial.py
 step t_tpbwr.log 300 $PYT tests/test_gpu_fullsize.py -k "receiver_major or edgeless or no_edges"
 step t_model.log 600 $PYT tests/test_gpu_parity.py -k "model_forward_backward_matches_oracle or other_radial"
 step t_bf16.log 400 $PYT tests/test_gpu_bf16.py
