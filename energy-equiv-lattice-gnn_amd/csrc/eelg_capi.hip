@@ -486,24 +486,6 @@ int eelg_tp_bwd_sorted(int cfg, const float* x, const float* sh, const float* w,
   return check_launch("tp_bwd");
 }
 
-// receiver-major streaming backward: node tiles as tp_fwd, nbgroups (l1) blocks per tile
-int eelg_tp_bwd_csr(int cfg, const float* x, const float* sh, const float* w, const int* sender,
-                    const int* rowptr, int n_nodes, const float* grad_agg, float inv_norm,
-                    float* grad_w, float* gxe, void* stream) {
-  const eelg_tp_cfg* c = tp_cfg(cfg);
-  if (!c) return -1;
-  if (n_nodes <= 0) return 0;
-  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(sh) |
-        reinterpret_cast<uintptr_t>(w)) & 15) != 0)
-    return fail(-2, "tp_bwd_csr: x, sh and w must be 16-byte aligned");
-  const int tn = 2 * c->fwpb * c->nph;
-  const int tiles = (n_nodes + tn - 1) / tn;
-  hipLaunchKernelGGL(c->bwr, dim3(((tiles + 7) / 8) * 8 * c->nbgroups), dim3(64 * c->fwpb), 0,
-                     (hipStream_t)stream, x, sh, w, sender, rowptr, n_nodes, grad_agg, inv_norm,
-                     grad_w, gxe);
-  return check_launch("tp_bwd_csr");
-}
-
 int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
                 const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                 float* grad_w, float* gxe, void* stream) {

@@ -15,8 +15,6 @@ typedef void (*eelg_tp_bwd_bf_fn)(const float*, const float*, const unsigned sho
                                   unsigned short*, const int*);
 // sender-order backward: (x, sh, w, sperm, srowptr, receiver, n_nodes, grad_agg, inv_norm,
 // grad_w, grad_x)
-typedef void (*eelg_tp_bwr_fn)(const float*, const float*, const float*, const int*, const int*, int,
-                               const float*, float, float*, float*);
 typedef void (*eelg_tp_bws_fn)(const float*, const float*, const float*, const int*, const int*,
                                const int*, int, const float*, float, float*, float*);
 typedef void (*eelg_tp_bws_bf_fn)(const float*, const float*, const unsigned short*, const int*,
@@ -41,7 +39,6 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_bf_fn bwd_bf;
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
-  eelg_tp_bwr_fn bwr;        // receiver-major streaming backward (fp32)
 };
 
 struct eelg_sc_cfg {
@@ -56,7 +53,7 @@ struct eelg_sc_cfg {
   int nbc;                       // nodes per coef-grad staged tile (chunk granularity)
   int nb;                        // nodes per fwd / grad-x workgroup
   int nth;                       // threads per fwd / grad-x workgroup
-  int cld;                       // coefficient row stride (nterms rounded up to whole DMA chunks)
+  int cld;                       // coefficient row stride (nterms rounded up to 16: 64-B aligned rows)
 };
 
 const eelg_tp_cfg* eelg_tp_table(int* n);

@@ -51,18 +51,14 @@ TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
 TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
-# symmetric contraction: terms per pinned block (a scheduling region: the pins keep hipcc from
-# hoisting the monomials of later blocks), forward / grad-x
+# symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
+# computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
+# 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
+# 1 ahead, it spills SGPRs beyond)
+SC_PFD_FWD = int(os.environ.get("EELG_SC_PFD_FWD", "1"))
 SC_BLOCK_FWD = int(os.environ.get("EELG_SC_BLOCK_FWD", "32"))
+SC_PFD_BWD = int(os.environ.get("EELG_SC_PFD_BWD", "1"))
 SC_BLOCK_BWD = int(os.environ.get("EELG_SC_BLOCK_BWD", "64"))
-# fwd / grad-x: the coefficient stream.  Each wave's channel row of coefficients travels by
-# LDS-DMA (global_load_lds_dwordx4) in chunks of SC_CCH terms into a per-wave ring of
-# SC_CSLOTS slots; the polynomial reads them as 4-term quads (ds_read_b128, a wave-uniform
-# broadcast) SC_CD quads ahead of use.  The coefficient row stride is padded to a multiple of
-# SC_CCH (sc config coef_ld).
-SC_CCH = int(os.environ.get("EELG_SC_CCH", "128"))
-SC_CSLOTS = int(os.environ.get("EELG_SC_CSLOTS", "3"))
-SC_CD = int(os.environ.get("EELG_SC_CD", "4"))
 # fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
 # consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
 SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
@@ -505,191 +501,6 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     return L
 
 
-def _emit_tp_bwd_rmaj(name, bgroups, din, nshp, dmid, wn, node_off) -> List[str]:
-    """tp_bwd in receiver-major streaming form ("tp_bwr"): the mapping, grid and LDS-DMA edge
-    pipeline of the forward (_emit_tp_fwd_glds2: a half-wave owns TP_NPH consecutive receivers
-    and streams their in-edges, the x / SH / weight rows of edges e+1 and e+2 in flight by
-    LDS-DMA), over the backward's l1 groups (each owns a disjoint slice of gxe).  A receiver's
-    grad_agg slices are loaded into registers once, when its first in-edge comes up, instead of
-    once per in-edge; per edge the lanes write grad_w of the group's paths and the group's gxe
-    slice (exec-masked to the half-waves that still have edges).  Same arithmetic as tp_bwd
-    (bitwise-equal results)."""
-    WPB = TP_FWD_WPB
-    TN = 2 * WPB * TP_NPH
-    ng = len(bgroups)
-    glist = _glds_chunks(bgroups, nshp, node_off, 4)
-    NJ = max(-(-len(g[2]) // 64) for g in glist)
-    NI = NJ * 64
-    L: List[str] = []
-    L.append(f"__global__ __launch_bounds__({64 * WPB}) void tp_bwr_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ sh, const float* __restrict__ w,")
-    L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
-    L.append("    const float* __restrict__ gagg, float inv_norm, float* __restrict__ gw,")
-    L.append("    float* __restrict__ gxe) {")
-    L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
-    L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5;")
-    L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-    L.append(f"  const int u = lane & {MUL - 1};")
-    L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
-    L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-    L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
-    L.append(f"  const int nw0 = (tile * {WPB} + wv) * {2 * TP_NPH};")
-    L.append("  if (nw0 >= n_nodes) return;   // uniform per wave")
-    L.append("  float4* __restrict__ ib = &img_[wv][0][0][0];")
-    L.append("  const char* pad_ = reinterpret_cast<const char*>(eelg_tp_pad);")
-    L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)ib);")
-    for h in (0, 1):
-        L.append(f"  const int n0_{h} = min(nw0 + {h * TP_NPH}, n_nodes), n1_{h} = min(n0_{h} + {TP_NPH}, n_nodes);")
-        L.append(f"  int e_{h} = rowptr[n0_{h}];")
-        L.append(f"  const int eend_{h} = rowptr[n1_{h}];")
-        L.append(f"  int node_{h} = n0_{h}, nend_{h} = rowptr[min(n0_{h} + 1, n1_{h})], "
-                 f"nend2_{h} = rowptr[min(n0_{h} + 2, n1_{h})], gn_{h} = -1;")
-    L.append("  switch (grp) {")
-    for gi, grp in enumerate(bgroups):
-        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
-        assert len(need_l1) == 1
-        l1 = need_l1[0]
-        d1 = 2 * l1 + 1
-        nj = -(-len(chunks) // 64)
-        L.append(f"  case {gi}: {{ // input block l1 = {l1}: {len(chunks)} chunks of 16 B per half-wave and edge")
-        L += _glds_desc(chunks, nj)
-
-        def issue(buf, ahead):
-            out = ["    {"]
-            for h in (0, 1):
-                out.append(f"      {{ const bool ok_ = e_{h} + {ahead} < eend_{h};")
-                out.append(f"        const int ee_ = ok_ ? e_{h} + {ahead} : 0;")
-                out.append(f"        const int ss_ = *(ok_ ? sender + ee_ : reinterpret_cast<const int*>(pad_));   // never a load through a null sender (E = 0)")
-                out.append(f"        const char* xb = ok_ ? reinterpret_cast<const char*>(x + (size_t)ss_ * {din}) : pad_;")
-                out.append(f"        const char* shb = ok_ ? reinterpret_cast<const char*>(sh + (size_t)ee_ * {nshp}) : pad_;")
-                out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")
-                out.append(f"        float4* dst = ib + ({buf}) * {2 * NI} + {h * NI};")
-                for j in range(nj):
-                    out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
-                               f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
-                               f"(__attribute__((address_space(3))) void*)(dst + {64 * j}), 16, 0, 0);")
-                out.append("      }")
-            out.append("    }")
-            return out
-        gregs = [f"g{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
-        L.append("    float " + ", ".join(f"{g} = 0.0f" for g in gregs) + ";")
-        # vector stores per edge: one per path (grad_w) + the gxe slice's vector stores
-        nst = len(grp) + len(vec_store([f"gx{i}" for i in range(d1)], "o", "0"))
-        L += issue("0", 0)
-        L += issue("1", 1)
-        L.append("    int b = 0, it_ = 0;")
-        L.append("    for (;;) {")
-        # edge e's rows landed.  Vector memory operations complete in issue order on gfx9, and in
-        # the steady state edge e's LDS-DMA is followed by the stores of edge e-2, edge e+1's
-        # LDS-DMA and the stores of edge e-1; the first two edges wait for fewer (the counts must
-        # never exceed what is in flight behind the awaited DMA)
-        L.append(f'      if (it_ >= 2) asm volatile("s_waitcnt vmcnt({2 * nj + 2 * nst})" ::: "memory");')
-        L.append(f'      else if (it_ == 1) asm volatile("s_waitcnt vmcnt({2 * nj})" ::: "memory");')
-        L.append('      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-        L.append("      ++it_;")
-        L.append(f"      const unsigned imb = lds0 + b * {2 * NI * 16} + hf * {NI * 16};")
-        cur = ([f"x{l1}_{i}" for i in range(d1)]
-               + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
-               + [f"w{p.slot}" for p in grp])
-        L.append("      float " + ", ".join(cur) + ";")
-        tdecl = [f"tx{l1}_{i}" for i in range(0, 2 * l1, 2)]
-        if tdecl:
-            L.append("      eelg_f2r " + ", ".join(tdecl) + ";")
-        need_y = sorted({l * l + j for l in need_l2 for j in range(2 * l + 1)})
-        L.append("      eelg_f4r " + ", ".join(f"ty{blk}" for blk in sorted({j // 4 for j in need_y})) + ";")
-        live, after = [], []
-        L.append(f"      {{ const unsigned xa = imb + 4 * ({fo_x[l1]} + u * {d1});")
-        i = 0
-        while i < d1:
-            if i + 1 < d1:
-                L.append(f"        asm volatile(\"ds_read2_b32 %0, %1 offset0:{i} offset1:{i + 1}\" : \"=v\"(tx{l1}_{i}) : \"v\"(xa));")
-                live.append(f"tx{l1}_{i}")
-                after.append(f"x{l1}_{i} = tx{l1}_{i}[0]; x{l1}_{i + 1} = tx{l1}_{i}[1];")
-                i += 2
-            else:
-                L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * i}\" : \"=v\"(x{l1}_{i}) : \"v\"(xa));")
-                live.append(f"x{l1}_{i}")
-                i += 1
-        L.append("      }")
-        for blk in sorted({j // 4 for j in need_y}):
-            L.append(f"      asm volatile(\"ds_read_b128 %0, %1 offset:{4 * fo_sh + 16 * blk}\" : \"=v\"(ty{blk}) : \"v\"(imb));")
-            live.append(f"ty{blk}")
-            after.append(" ".join(f"y{j} = ty{blk}[{j - 4 * blk}];" for j in need_y if j // 4 == blk))
-        L.append("      { const unsigned wa = imb + 4 * u;")
-        for p in grp:
-            L.append(f"        asm volatile(\"ds_read_b32 %0, %1 offset:{4 * fo_w[p.slot]}\" : \"=v\"(w{p.slot}) : \"v\"(wa));")
-            live.append(f"w{p.slot}")
-        L.append("      }")
-        for k in range(0, len(live), 24):
-            ops = ", ".join(f'"+v"({v})' for v in live[k: k + 24])
-            L.append(f'      asm volatile("s_waitcnt lgkmcnt(0)" : {ops} : : "memory");')
-        L += ["      " + a_ for a_ in after]
-        L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
-        # receivers whose in-edges are done (and receivers with none) are skipped
-        for h in (0, 1):
-            L.append(f"      while (node_{h} < n1_{h} && nend_{h} == e_{h}) {{   // uniform")
-            L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
-            L.append("      }")
-        L.append("      if (e_0 >= eend_0 && e_1 >= eend_1) break;")
-        # the current receiver's grad_agg slices, when it changed (lanes of that half only)
-        L.append("      { const bool c0_ = e_0 < eend_0 && node_0 != gn_0, c1_ = e_1 < eend_1 && node_1 != gn_1;")
-        L.append("        if (c0_ || c1_) {   // uniform")
-        L.append("          if (hf ? c1_ : c0_) {")
-        L.append(f"            const float* __restrict__ ge = gagg + (size_t)(hf ? node_1 : node_0) * {dmid};")
-        for p in grp:
-            d3 = 2 * p.l3 + 1
-            L += ["            " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
-                                                        f"{p.out_off} + u * {d3}")]
-        L.append("          }")
-        L.append("          if (c0_) gn_0 = node_0;")
-        L.append("          if (c1_) gn_1 = node_1;")
-        L.append("        }")
-        L.append("      }")
-        L += ["  " + ln for ln in issue("b", 2)]
-        # edge e of this lane's half: grad_w of the group's paths and the gxe slice
-        L.append("      const int em_ = hf ? e_1 : e_0;")
-        L.append("      const bool st_ = em_ < (hf ? eend_1 : eend_0);")
-        L.append(f"      float* __restrict__ gwe = gw + (size_t)em_ * {wn} + u;")
-        for i in range(d1):
-            L.append(f"      float gx{i} = 0.0f;")
-        base_pin = cur + [f"gx{i}" for i in range(d1)] + gregs
-        for p in grp:
-            d3 = 2 * p.l3 + 1
-            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-            L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
-            byik: Dict[Tuple[int, int], List[str]] = {}
-            for (i, j, k), c in _path_cg(p):
-                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
-            for (i, k), ts in byik.items():
-                L.append(f"        const float m{i}_{k} = {' + '.join(ts)};")
-            gterms = []
-            for k in range(d3):
-                ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
-                if ts:
-                    gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
-            gexpr = " + ".join(gterms) if gterms else "0.0f"
-            L.append(f"        if (st_) gwe[{p.slot * MUL}] = cp * ({gexpr});")
-            L.append(f"        const float hw = cp * w{p.slot};")
-            for i in range(d1):
-                ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
-                if ts:
-                    L.append(f"        gx{i} = fmaf(hw, {' + '.join(ts)}, gx{i});")
-            L.append("      }")
-            L.append("      " + pin(base_pin))
-        L.append("      if (st_) {")
-        L.append(f"        float* __restrict__ o = gxe + (size_t)em_ * {din};")
-        L += ["        " + ln for ln in vec_store([f"gx{i}" for i in range(d1)], "o", f"{node_off[l1]} + u * {d1}")]
-        L.append("      }")
-        L.append("      ++e_0; ++e_1; b ^= 1;")
-        L.append("    }")
-        L.append('    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the wave')
-        L.append("    break; }")
-    L.append("  default: break;")
-    L.append("  }")
-    L.append("}")
-    return L
-
-
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -962,9 +773,6 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  }")
     L.append("}")
 
-    if not bf:
-        L += _emit_tp_bwd_rmaj(name, bgroups, din, nshp, dmid, wn, node_off)
-
     # ---------------- backward in sender order ----------------
     # One half-wave owns one SENDER node and walks its out-edges through the sender CSR
     # (srowptr / sperm): x[sender] is loaded once, grad_x is summed in registers and stored
@@ -1195,88 +1003,6 @@ def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> L
     return out
 
 
-class CoefStream:
-    """Emitter of a wave's coefficient stream (fwd / grad-x of the contraction).
-
-    Chunk k (terms [k*ch, (k+1)*ch) of the wave's channel row) is moved by ONE LDS-DMA
-    instruction (ch/4 lanes x 16 B) into ring slot k % S; the DMAs of chunks 0..S-1 are issued
-    at kernel start, and the DMA of chunk k+S once every read of chunk k has completed.  The
-    straight-line polynomial reads 4-term quads with inline-asm ds_read_b128 (wave-uniform
-    address: a broadcast) ``ahead`` quads before the quad it needs and waits with counted
-    ``s_waitcnt lgkmcnt`` (LDS reads of a wave return in order); a chunk's first read waits
-    with a counted ``s_waitcnt vmcnt`` that leaves the later chunks' DMAs in flight (vector
-    loads return in order).  The reads are asm because hipcc would otherwise order every LDS
-    read after ALL outstanding LDS-DMA (it models a DMA as writing 16 B at the slot base,
-    see DESIGN 3.3).  Each quad register is threaded through its wait ("+v") before any use."""
-
-    def __init__(self, nt: int, ch: int, slots: int, ahead: int, nwaves: int):
-        assert ch in (128, 256) and slots >= 2 and 1 <= ahead <= 12
-        self.nt, self.ch, self.S, self.D, self.NW = nt, ch, slots, ahead, nwaves
-        self.nq = (nt + 3) // 4
-        self.nchunk = -(-nt // ch)
-        self.issued = 0          # quads [0, issued) have their read issued
-        self.waited = 0          # quads [0, waited) have completed
-        self.ready = 0           # chunks [0, ready) have landed in LDS (vmcnt waited)
-        self.dmas = 0            # chunks [0, dmas) have their DMA issued
-        self.released = 0        # chunks [0, released) are fully read (slot reusable)
-
-    def decl(self) -> List[str]:
-        return [f"  __shared__ float4 cring_[{self.NW}][{self.S}][{self.ch // 4}];   // per-wave coefficient ring"]
-
-    def prologue(self) -> List[str]:
-        out = ["  const int wvu_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);",
-               "  const unsigned crb_ = (unsigned)(size_t)((__attribute__((address_space(3))) float4*)&cring_[wvu_][0][0]);"]
-        for j0 in range(0, self.nq, 32):   # quads are assigned inside nested scopes, declared here
-            out.append("  eelg_f4r " + ", ".join(f"cq{j}" for j in range(j0, min(j0 + 32, self.nq))) + ";")
-        for _ in range(min(self.S, self.nchunk)):
-            out += self._dma()
-        return out
-
-    def _dma(self) -> List[str]:
-        k = self.dmas
-        self.dmas += 1
-        guard = "if (lane < 32) " if self.ch == 128 else ""
-        return [f"  {guard}__builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
-                f"(cf + {k * self.ch} + 4 * lane), (__attribute__((address_space(3))) void*)"
-                f"&cring_[wvu_][{k % self.S}][0], 16, 0, 0);   // coefficient chunk {k}"]
-
-    def _issue(self) -> List[str]:
-        j = self.issued
-        k = 4 * j // self.ch
-        out = []
-        if k >= self.ready:
-            assert k == self.ready and k < self.dmas
-            out.append(f'  asm volatile("s_waitcnt vmcnt({self.dmas - 1 - k})" ::: "memory");   // chunk {k} landed')
-            self.ready += 1
-        off = 4 * ((k % self.S) * self.ch + (4 * j) % self.ch)
-        out.append(f'  asm volatile("ds_read_b128 %0, %1 offset:{off}" : "=v"(cq{j}) : "v"(crb_));')
-        self.issued += 1
-        return out
-
-    def use(self, t: int) -> List[str]:
-        """lines to emit before the first use of term t"""
-        j = t // 4
-        if j < self.waited:
-            return []
-        out = []
-        while self.issued <= min(j + self.D, self.nq - 1):
-            out += self._issue()
-        done = list(range(self.waited, j + 1))
-        ops = ", ".join(f'"+v"(cq{q})' for q in done)
-        out.append(f'  asm volatile("s_waitcnt lgkmcnt({self.issued - 1 - j})" : {ops} : : "memory");')
-        self.waited = j + 1
-        # chunks whose every quad has completed: their slot takes chunk k + S
-        while self.released < self.nchunk and min(self.nq, (self.released + 1) * self.ch // 4) <= self.waited:
-            self.released += 1
-            if self.dmas < self.nchunk:
-                out += self._dma()
-        return out
-
-    @staticmethod
-    def c(t: int) -> str:
-        return f"cq{t // 4}[{t % 4}]"
-
-
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
     """Symmetric contraction kernels.
 
@@ -1316,7 +1042,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         TP += 1                             # odd -> conflict-free lane rows
     drow, orow = lin.row, lout.row
     nt = len(plan.terms)
-    cld = -(-nt // SC_CCH) * SC_CCH          # coefficient row stride: whole LDS-DMA chunks
+    cld = -(-nt // 16) * 16                  # coefficient row stride: 64-B aligned channel rows
 
     def lq(lay, a, cl):
         """LDS column of component a for channel-in-quad cl (may be a runtime expr)."""
@@ -1450,10 +1176,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[{NB} * {TP}];")
-    cs = CoefStream(nt, SC_CCH, SC_CSLOTS, SC_CD, NTH // 64)
-    L += cs.decl()
     L += head
-    L += cs.prologue()
     L += stage_in("x", "tile", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
@@ -1463,30 +1186,33 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  float o{q} = 0.0f;")
     blocks = sc_blocks(plan, SC_BLOCK_FWD)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    C = CoefStream.c
+    for b0 in blocks[:SC_PFD_FWD]:
+        for t in b0["terms"]:
+            L.append(f"  float c{t} = cf[{t}];")
     for bi, blk in enumerate(blocks):
+        # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
+        for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
+            L.append(f"  float c{t} = cf[{t}];")
+        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L += cs.use(t)
-                L.append(f"  o{q} = fmaf({C(t)}, x{a}, o{q});")
+                L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv = f"p{a}_{b}"
             if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b};")
             for t, q in sg["d2"]:
-                L += cs.use(t)
-                L.append(f"  o{q} = fmaf({C(t)}, {pv}, o{q});")
+                L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
             for cc, lst in sg["d3"]:
                 L.append(f"  {{ const float m = {pv} * x{cc};")
                 for t, q in lst:
-                    L += cs.use(t)
-                    L.append(f"    o{q} = fmaf({C(t)}, m, o{q});")
+                    L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
                 L.append("  }")
             if not sg["last"]:
                 carry = [pv]
-        L.append("  " + pin(fv + carry))
+        L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for q in range(Dout):
         L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
@@ -1504,10 +1230,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     # separate x / grad_out tiles.  When xt / gt are given, the staged tiles are also written
     # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
     L.append(f"  __shared__ float tx[{NB} * {TP}];")
-    cs = CoefStream(nt, SC_CCH, SC_CSLOTS, SC_CD, NTH // 64)
-    L += cs.decl()
     L += head
-    L += cs.prologue()
     L += stage_in("x", "tx", lin, NB, NTH)
     L.append("  __syncthreads();")
     L.append("  if (xt) {")
@@ -1527,31 +1250,35 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     blocks = sc_blocks(plan, SC_BLOCK_BWD)
+    for b0 in blocks[:SC_PFD_BWD]:
+        for t in b0["terms"]:
+            L.append(f"  float c{t} = cf[{t}];")
     for bi, blk in enumerate(blocks):
+        # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
+        for t in (blocks[bi + SC_PFD_BWD]["terms"] if bi + SC_PFD_BWD < len(blocks) else []):
+            L.append(f"  float c{t} = cf[{t}];")
+        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_BWD] for t in b1["terms"]]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L += cs.use(t)
-                L.append(f"  d{a} = fmaf({C(t)}, g{q}, d{a});")
+                L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv, sv = f"p{a}_{b}", f"s{a}_{b}"
             if sg["first"]:
                 L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
             for t, q in sg["d2"]:
-                L += cs.use(t)
-                L.append(f"  {sv} = fmaf({C(t)}, g{q}, {sv});")
+                L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
             for cc, lst in sg["d3"]:
                 L.append("  { float s = 0.0f;")
                 for t, q in lst:
-                    L += cs.use(t)
-                    L.append(f"    s = fmaf({C(t)}, g{q}, s);")
+                    L.append(f"    s = fmaf(c{t}, g{q}, s);")
                 L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
             if sg["last"]:
                 L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
             else:
                 carry = [pv, sv]
-        L.append("  " + pin(bv + carry))
+        L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for a in range(D):
         L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
@@ -1756,7 +1483,7 @@ def main(outdir: str) -> None:
         lmax = int(name.split("_l")[1])
         parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                      f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw, tp_bwr_{name}}},')
+                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
     parts.append("};")
     parts.append("static const eelg_sc_cfg kScConfigs[] = {")
     for name, i in sc_table:

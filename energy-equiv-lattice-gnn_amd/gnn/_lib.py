@@ -58,7 +58,6 @@ _SIGS = {
     "eelg_linear_pack_size": ([_P], ctypes.c_longlong),
     "eelg_linear_pack": ([_P, _P, _P, _P], _I),
     "eelg_linear_fwd_pk": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
-    "eelg_tp_bwd_csr": ([_I, _P, _P, _P, _P, _P, _I, _P, ctypes.c_float, _P, _P, _P], _I),
     "eelg_split_bf16x3": ([_P, ctypes.c_longlong, _P, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),

@@ -25,8 +25,12 @@ from .irreps import Irreps
 LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
 LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "64"))
 # forward / grad-x of the eligible linears on bf16 MFMA with fp32-accurate split operands (1),
-# or on the fp32 MFMA kernels (0)
+# or on the fp32 MFMA kernels (0).  Only descriptors whose every slot sums K >= LIN_X6_MINK take
+# it: r04b kbench, 7360->800 fwd (K 160..320) 0.261 vs 0.290 ms fp32; K = 32 (the 800->800
+# linears, every grad-x of the 7360->800) 0.056-0.391 vs 0.050-0.325 ms -- one 32-wide chunk per
+# group leaves the split and LDS B-fragment reads unamortised
 LIN_X6 = os.environ.get("EELG_LIN_X6", "1") != "0"
+LIN_X6_MINK = int(os.environ.get("EELG_LIN_X6_MINK", "128"))
 # the readout Gate as fused HIP passes (1) or torch elementwise ops (0)
 GATE_FUSED = os.environ.get("EELG_GATE_FUSED", "1") != "0"
 
@@ -252,7 +256,8 @@ class Linear(torch.nn.Module):
                 return False
             if sl.bias_off >= 0 and sl.d != 1:
                 return False
-            if sum(sl.src[t].k for t in range(sl.n_src)) > 320:
+            ks = sum(sl.src[t].k for t in range(sl.n_src))
+            if ks > 320 or ks < LIN_X6_MINK:
                 return False
             for t in range(sl.n_src):
                 if sl.src[t].k % 32 or sl.src[t].x_off % 4:

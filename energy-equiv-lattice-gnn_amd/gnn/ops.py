@@ -66,9 +66,6 @@ SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
 # results; measured equal (r02s3: sender sum 169 -> 137 us, tp_bwd 1036 -> 1128 us from the
 # scattered row stores; 1844 / 1855 vs 1844 / 1847 graphs/s), so off by default.
 TP_BWD_SPOS = os.environ.get("EELG_TP_BWD_SPOS", "0") != "0"
-# fp32 edge-order backward in receiver-major streaming form (eelg_tp_bwd_csr: each receiver's
-# grad_agg slices read once, edge rows by LDS-DMA; bitwise-equal to eelg_tp_bwd)
-TP_BWD_RMAJ = os.environ.get("EELG_TP_BWD_RMAJ", "1") != "0"
 _TBS = os.environ.get("EELG_TP_BWD_SENDER", "auto")
 TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
@@ -367,15 +364,6 @@ class _TPInteraction(torch.autograd.Function):
             TIMER.stop(tok)
             return gx, None, gw, None, None, None, None
         gxe = torch.empty(e, info["din"], device=x.device, dtype=w.dtype)
-        if TP_BWD_RMAJ and w.dtype == torch.float32 and not TP_BWD_SPOS and csr.num_nodes > 0:
-            tok = TIMER.start(f"tp_bwd[din={info['din']}]")
-            _lib.check(lib.eelg_tp_bwd_csr(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w),
-                                           _lib.ptr(csr.sender), _lib.ptr(csr.rowptr),
-                                           csr.rowptr.shape[0] - 1, _lib.ptr(g), float(ctx.inv_norm),
-                                           _lib.ptr(gw), _lib.ptr(gxe), _lib.stream(gxe)), "tp_bwd_csr")
-            TIMER.stop(tok)
-            gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
-            return gx, None, gw, None, None, None, None
         spos = csr.sender_pos() if TP_BWD_SPOS else None
         bwd = lib.eelg_tp_bwd_sorted_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_sorted
         tok = TIMER.start(f"tp_bwd[din={info['din']}]")

@@ -40,7 +40,7 @@ int eelg_tp_info(int cfg, int* info7, uint64_t* sig);
  * (D: coupling components per channel of the input, D_out: of the output; they differ when the
  * product maps the SH-lmax interaction irreps onto wider hidden irreps; coef_chunk: the node
  * chunk of eelg_sc_bwd_coef; coef_ld: the row stride of the coefficient matrix, nterms rounded
- * up to the kernels' coefficient DMA chunk, a multiple of 128) */
+ * up to a multiple of 16, so every channel row starts on a 64-byte line) */
 int eelg_sc_find(const char* name);
 int eelg_sc_info(int cfg, int* info8, uint64_t* sig);
 
@@ -66,15 +66,6 @@ int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const 
 int eelg_tp_bwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
                 const int* receiver, int n_edges, const float* grad_agg, float inv_norm,
                 float* grad_w, float* gxe, void* stream);
-
-/* eelg_tp_bwd in receiver-major streaming form: the same grad_w [E, weight_numel] and per-edge
- * gxe [E, din] (receiver-sorted edge order), from the receiver CSR (rowptr [n_nodes + 1], as
- * eelg_tp_fwd) instead of per-edge receiver indices.  Each receiver's grad_agg slices are read
- * once, and the x / SH / weight rows of the next two edges travel by LDS-DMA: x, sh and w must
- * be 16-byte aligned (-2 otherwise).  Bitwise-equal to eelg_tp_bwd. */
-int eelg_tp_bwd_csr(int cfg, const float* x, const float* sh, const float* w, const int* sender,
-                    const int* rowptr, int n_nodes, const float* grad_agg, float inv_norm,
-                    float* grad_w, float* gxe, void* stream);
 
 /* BASELINE config 5 (bf16 storage, fp32 arithmetic): eelg_tp_fwd / eelg_tp_bwd with the
  * edge-sized tensors w, grad_w [E, weight_numel] and gxe [E, din] held as bf16 bit patterns

@@ -305,3 +305,14 @@ def test_reshape_irreps_round_trip_matches_reference_layout():
     assert r.shape == (7, 32, 25)
     assert torch.equal(r, oreshape("32x0e+32x1o+32x2e+32x3o+32x4e", x))
     assert torch.equal(unreshape_irreps(ir, r), x)
+
+
+def test_packed_linear_rule_keeps_short_k_on_fp32_kernels():
+    """The split-bf16 linear kernel is chosen only where every output slot sums K >= 128 (the
+    7360 -> 800 forward); K = 32 descriptors (800 -> 800, every grad-x) stay on the fp32 kernels,
+    which measured faster there (o3.LIN_X6_MINK)."""
+    from gnn import o3
+    big = o3.Linear("160x0e+256x1o+320x2e+320x3o+288x4e", "32x0e+32x1o+32x2e+32x3o+32x4e")
+    assert big._pk_ok == {"fwd": True, "bx": False}
+    sq = o3.Linear("32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+32x1o+32x2e+32x3o+32x4e")
+    assert sq._pk_ok == {"fwd": False, "bx": False}

@@ -129,14 +129,6 @@ def main():
                                        ops._lib.stream(x)), "tp_bwd")
     bwd_bytes = 4 * (n * 800 + e * 25 + 2 * e * info["wn"] + 2 * e + e * 800 + n * info["dmid"])
     rec("tp_bwd (B)", timeit_if("tp_bwd (B)", tpb, args.reps), bwd_bytes, 2 * tp_flops)
-    if hasattr(lib, "eelg_tp_bwd_csr"):
-        def tpbr():
-            ops._lib.check(lib.eelg_tp_bwd_csr(idx, ops._lib.ptr(x), ops._lib.ptr(sh), ops._lib.ptr(w),
-                                               ops._lib.ptr(csr.sender), ops._lib.ptr(csr.rowptr), n,
-                                               ops._lib.ptr(g), 0.25, ops._lib.ptr(gw), ops._lib.ptr(gxe),
-                                               ops._lib.stream(x)), "tp_bwd_csr")
-        rec("tp_bwd_csr (B, receiver-major)", timeit_if("tp_bwd_csr (B, receiver-major)", tpbr, args.reps),
-            bwd_bytes, 2 * tp_flops)
     rec("segment_sum gxe->gx (800)", timeit_if("segment_sum gxe->gx (800)", lambda: ops.segment_sum_csr(gxe, csr.srowptr, n, idx=csr.sperm), args.reps),
         4 * (e * 800 + n * 800 + 2 * e))
     m7360 = torch.randn(e, 7360, device=dev)
