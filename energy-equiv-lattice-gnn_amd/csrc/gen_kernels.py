@@ -62,6 +62,14 @@ SC_BLOCK_BWD = int(os.environ.get("EELG_SC_BLOCK_BWD", "64"))
 # fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
 # consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
 SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
+# fwd / grad-x: two nodes per lane (rows lane and lane + 64 of a 128-node tile) on packed f32
+# VALU (v_pk_fma_f32 / v_pk_mul_f32, the coefficient broadcast from its SGPR): twice the FMAs
+# per issued instruction and per coefficient load (tools/proto/pkfma_bench.hip, r04c: v_fma_f32
+# 41 / 60 / 67 TFLOP/s at 1 / 2 / 4 waves per SIMD, v_pk_fma_f32 81 / 116 / 130)
+SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+# waves per SIMD asked of the packed forward / grad-x (amdgpu_waves_per_eu; 0 = the compiler's choice)
+SC_PK_WPE_FWD = int(os.environ.get("EELG_SC_PK_WPE_FWD", "0"))
+SC_PK_WPE_BWD = int(os.environ.get("EELG_SC_PK_WPE_BWD", "0"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, the most
 # accumulators (terms) per wave
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
@@ -1064,8 +1072,24 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    NB = 64 * SC_NT                         # nodes per workgroup (fwd / grad-x), one per lane
-    NTH = 256 * SC_NT                       # threads per workgroup (fwd / grad-x)
+    PK = bool(SC_PK)
+    NB = 128 if PK else 64 * SC_NT          # nodes per workgroup (fwd / grad-x): one or two per lane
+    NTH = 256 if PK else 256 * SC_NT        # threads per workgroup (fwd / grad-x)
+    VT = "eelg_f2" if PK else "float"       # a lane's value type: its node pair or its node
+
+    def vfma(a, b, c):
+        return f"__builtin_elementwise_fma({a}, {b}, {c})" if PK else f"fmaf({a}, {b}, {c})"
+
+    def cfma(t, b, c):
+        """c += coefficient t * b (the coefficient is a wave-uniform SGPR, broadcast)"""
+        return vfma(f"(eelg_f2)(c{t})", b, c) if PK else vfma(f"c{t}", b, c)
+    zero = "(eelg_f2)(0.0f)" if PK else "0.0f"
+
+    def lds_get(ptr, col):
+        return f"(eelg_f2){{{ptr}[{col}], {ptr}[64 * {TP} + {col}]}}" if PK else f"{ptr}[{col}]"
+
+    def lds_put(ptr, col, v):
+        return f"{ptr}[{col}] = {v}.x; {ptr}[64 * {TP} + {col}] = {v}.y;" if PK else f"{ptr}[{col}] = {v};"
 
     # Staging between the mul-major rows and the quad tile.  A quad owns, per node and l-block,
     # one run of 4*d floats (d float4, 16-B aligned), so a tile of nb nodes is nb * D float4:
@@ -1164,7 +1188,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 f"  const int cq = rest_ % {NQ};",
                 f"  const int n0 = ((rest_ / {NQ}) * 8 + xcd) * {nb};",
                 "  if (n0 >= n_nodes) return;   // uniform per workgroup (tile count padded to 8)"]
-    nrow = "lane" if SC_NT == 1 else "((wv >> 2) * 64 + lane)"   # this lane's node row in the tile
+    nrow = "lane" if SC_NT == 1 or PK else "((wv >> 2) * 64 + lane)"   # this lane's (first) node row in the tile
     head = tile_map(NB) + [
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
@@ -1172,7 +1196,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             f"  const float* __restrict__ cf = coef + (size_t)c * {cld};"]
 
     # ---------------- forward ----------------
-    L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
+    wpe = (lambda w: f" __attribute__((amdgpu_waves_per_eu({w})))" if PK and w else "")
+    L.append(f"__global__ __launch_bounds__({NTH}){wpe(SC_PK_WPE_FWD)} void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[{NB} * {TP}];")
@@ -1181,9 +1206,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  __syncthreads();")
     L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = tr[{lq(lin, a, 'cl')}];")
+        L.append(f"  {VT} x{a} = {lds_get('tr', lq(lin, a, 'cl'))};")
     for q in range(Dout):
-        L.append(f"  float o{q} = 0.0f;")
+        L.append(f"  {VT} o{q} = {zero};")
     blocks = sc_blocks(plan, SC_BLOCK_FWD)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
     for b0 in blocks[:SC_PFD_FWD]:
@@ -1197,32 +1222,32 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  o{q} = fmaf(c{t}, x{a}, o{q});")
+                L.append(f"  o{q} = {cfma(t, f'x{a}', f'o{q}')};")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv = f"p{a}_{b}"
             if sg["first"]:
-                L.append(f"  float {pv} = x{a} * x{b};")
+                L.append(f"  {VT} {pv} = x{a} * x{b};")
             for t, q in sg["d2"]:
-                L.append(f"  o{q} = fmaf(c{t}, {pv}, o{q});")
+                L.append(f"  o{q} = {cfma(t, pv, f'o{q}')};")
             for cc, lst in sg["d3"]:
-                L.append(f"  {{ const float m = {pv} * x{cc};")
+                L.append(f"  {{ const {VT} m = {pv} * x{cc};")
                 for t, q in lst:
-                    L.append(f"    o{q} = fmaf(c{t}, m, o{q});")
+                    L.append(f"    o{q} = {cfma(t, 'm', f'o{q}')};")
                 L.append("  }")
             if not sg["last"]:
                 carry = [pv]
         L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for q in range(Dout):
-        L.append(f"  tr[{lq(lout, q, 'cl')}] = o{q};")
+        L.append(f"  {lds_put('tr', lq(lout, q, 'cl'), f'o{q}')}")
     L.append("  __syncthreads();")
     L += stage_out("out", "tile", lout, NB, NTH)
     L.append("}")
 
 
     # ---------------- backward w.r.t. x ----------------
-    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}){wpe(SC_PK_WPE_BWD)} void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
     L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
@@ -1238,8 +1263,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append(f"  float* __restrict__ xr = tx + {nrow} * {TP};")
     for a in range(D):
-        L.append(f"  float x{a} = xr[{lq(lin, a, 'cl')}];")
-        L.append(f"  float d{a} = 0.0f;")
+        L.append(f"  {VT} x{a} = {lds_get('xr', lq(lin, a, 'cl'))};")
+        L.append(f"  {VT} d{a} = {zero};")
     L.append("  __syncthreads();")
     L += stage_in("gout", "tx", lout, NB, NTH)
     L.append("  __syncthreads();")
@@ -1247,7 +1272,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L += cm_store("gt", "tx", lout, NB, "    ", NTH)
     L.append("  }")
     for q in range(Dout):
-        L.append(f"  float g{q} = xr[{lq(lout, q, 'cl')}];")
+        L.append(f"  {VT} g{q} = {lds_get('xr', lq(lout, q, 'cl'))};")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     blocks = sc_blocks(plan, SC_BLOCK_BWD)
     for b0 in blocks[:SC_PFD_BWD]:
@@ -1261,27 +1286,27 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
-                L.append(f"  d{a} = fmaf(c{t}, g{q}, d{a});")
+                L.append(f"  d{a} = {cfma(t, f'g{q}', f'd{a}')};")
         for sg in blk.get("segs", []):
             a, b = sg["a"], sg["b"]
             pv, sv = f"p{a}_{b}", f"s{a}_{b}"
             if sg["first"]:
-                L.append(f"  float {pv} = x{a} * x{b}; float {sv} = 0.0f;")
+                L.append(f"  {VT} {pv} = x{a} * x{b}; {VT} {sv} = {zero};")
             for t, q in sg["d2"]:
-                L.append(f"  {sv} = fmaf(c{t}, g{q}, {sv});")
+                L.append(f"  {sv} = {cfma(t, f'g{q}', sv)};")
             for cc, lst in sg["d3"]:
-                L.append("  { float s = 0.0f;")
+                L.append(f"  {{ {VT} s = {zero};")
                 for t, q in lst:
-                    L.append(f"    s = fmaf(c{t}, g{q}, s);")
-                L.append(f"    d{cc} = fmaf(s, {pv}, d{cc}); {sv} = fmaf(s, x{cc}, {sv}); }}")
+                    L.append(f"    s = {cfma(t, f'g{q}', 's')};")
+                L.append(f"    d{cc} = {vfma('s', pv, f'd{cc}')}; {sv} = {vfma('s', f'x{cc}', sv)}; }}")
             if sg["last"]:
-                L.append(f"  d{a} = fmaf({sv}, x{b}, d{a}); d{b} = fmaf({sv}, x{a}, d{b});")
+                L.append(f"  d{a} = {vfma(sv, f'x{b}', f'd{a}')}; d{b} = {vfma(sv, f'x{a}', f'd{b}')};")
             else:
                 carry = [pv, sv]
         L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
     L.append("  __syncthreads();")
     for a in range(D):
-        L.append(f"  xr[{lq(lin, a, 'cl')}] = d{a};")
+        L.append(f"  {lds_put('xr', lq(lin, a, 'cl'), f'd{a}')}")
     L.append("  __syncthreads();")
     L += stage_out("gx", "tx", lin, NB, NTH)
     L.append("}")
@@ -1458,6 +1483,7 @@ def main(outdir: str) -> None:
              "typedef float eelg_f2u __attribute__((ext_vector_type(2), aligned(4)));",
              "typedef float eelg_f4a __attribute__((ext_vector_type(4)));",
              "typedef float eelg_f4r __attribute__((ext_vector_type(4)));",
+             "typedef float eelg_f2 __attribute__((ext_vector_type(2)));   // a lane's node pair (packed f32 VALU)",
              "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
