@@ -66,7 +66,11 @@ SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
 # VALU (v_pk_fma_f32 / v_pk_mul_f32, the coefficient broadcast from its SGPR): twice the FMAs
 # per issued instruction and per coefficient load (tools/proto/pkfma_bench.hip, r04c: v_fma_f32
 # 41 / 60 / 67 TFLOP/s at 1 / 2 / 4 waves per SIMD, v_pk_fma_f32 81 / 116 / 130)
-SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+SC_PK = int(os.environ.get("EELG_SC_PK", "0"))
+# fwd / grad-x: a block's coefficients are scalar-loaded as SGPR vectors (16 / 8 / 4 / 2 / 1
+# terms per s_load) and pinned as whole vectors, so the VALU reads them in place; 0 = one float
+# (and one pinned SGPR, hence an s_mov_b32 per term) per coefficient
+SC_CVEC = int(os.environ.get("EELG_SC_CVEC", "1"))
 # waves per SIMD asked of the packed forward / grad-x (amdgpu_waves_per_eu; 0 = the compiler's choice)
 SC_PK_WPE_FWD = int(os.environ.get("EELG_SC_PK_WPE_FWD", "0"))
 SC_PK_WPE_BWD = int(os.environ.get("EELG_SC_PK_WPE_BWD", "0"))
@@ -1082,7 +1086,33 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 
     def cfma(t, b, c):
         """c += coefficient t * b (the coefficient is a wave-uniform SGPR, broadcast)"""
-        return vfma(f"(eelg_f2)(c{t})", b, c) if PK else vfma(f"c{t}", b, c)
+        return vfma(f"(eelg_f2)({CE[t]})", b, c) if PK else vfma(CE[t], b, c)
+    CE: Dict[int, str] = {}                 # term -> expression of its (SGPR) coefficient
+
+    def cload(blk):
+        """the scalar loads of block blk's coefficients (a contiguous term range) and the names
+        to pin; records every term's coefficient expression in CE"""
+        ts = blk["terms"]
+        t0, n = ts[0], len(ts)
+        assert ts == list(range(t0, t0 + n))
+        if not SC_CVEC:
+            for t in ts:
+                CE[t] = f"c{t}"
+            return [f"  float c{t} = cf[{t}];" for t in ts], [f"c{t}" for t in ts]
+        out, names, t = [], [], t0
+        while t < t0 + n:
+            sz = next(z for z in (16, 8, 4, 2, 1) if z <= t0 + n - t)
+            nm = f"cv{t}"
+            if sz == 1:
+                out.append(f"  float {nm} = cf[{t}];")
+                CE[t] = nm
+            else:
+                out.append(f"  eelg_c{sz} {nm} = *reinterpret_cast<const eelg_c{sz}*>(cf + {t});")
+                for i in range(sz):
+                    CE[t + i] = f"{nm}[{i}]"
+            names.append(nm)
+            t += sz
+        return out, names
     zero = "(eelg_f2)(0.0f)" if PK else "0.0f"
 
     def lds_get(ptr, col):
@@ -1211,14 +1241,16 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  {VT} o{q} = {zero};")
     blocks = sc_blocks(plan, SC_BLOCK_FWD)
     fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    for b0 in blocks[:SC_PFD_FWD]:
-        for t in b0["terms"]:
-            L.append(f"  float c{t} = cf[{t}];")
+    pf = {}
+    for j in range(min(SC_PFD_FWD, len(blocks))):
+        lines, pf[j] = cload(blocks[j])
+        L += lines
     for bi, blk in enumerate(blocks):
         # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
-        for t in (blocks[bi + SC_PFD_FWD]["terms"] if bi + SC_PFD_FWD < len(blocks) else []):
-            L.append(f"  float c{t} = cf[{t}];")
-        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_FWD] for t in b1["terms"]]
+        if bi + SC_PFD_FWD < len(blocks):
+            lines, pf[bi + SC_PFD_FWD] = cload(blocks[bi + SC_PFD_FWD])
+            L += lines
+        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_FWD) for nm in pf.get(j, [])]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
@@ -1237,7 +1269,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 L.append("  }")
             if not sg["last"]:
                 carry = [pv]
-        L.append("  " + pin(fv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  " + pin(fv + carry, sgprs=nxt))
     L.append("  __syncthreads();")
     for q in range(Dout):
         L.append(f"  {lds_put('tr', lq(lout, q, 'cl'), f'o{q}')}")
@@ -1275,14 +1307,16 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append(f"  {VT} g{q} = {lds_get('xr', lq(lout, q, 'cl'))};")
     bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
     blocks = sc_blocks(plan, SC_BLOCK_BWD)
-    for b0 in blocks[:SC_PFD_BWD]:
-        for t in b0["terms"]:
-            L.append(f"  float c{t} = cf[{t}];")
+    pf = {}
+    for j in range(min(SC_PFD_BWD, len(blocks))):
+        lines, pf[j] = cload(blocks[j])
+        L += lines
     for bi, blk in enumerate(blocks):
         # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
-        for t in (blocks[bi + SC_PFD_BWD]["terms"] if bi + SC_PFD_BWD < len(blocks) else []):
-            L.append(f"  float c{t} = cf[{t}];")
-        nxt = [t for b1 in blocks[bi + 1: bi + 1 + SC_PFD_BWD] for t in b1["terms"]]
+        if bi + SC_PFD_BWD < len(blocks):
+            lines, pf[bi + SC_PFD_BWD] = cload(blocks[bi + SC_PFD_BWD])
+            L += lines
+        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_BWD) for nm in pf.get(j, [])]
         carry = []
         if blk["kind"] == "deg1":
             for t, a, q in blk["deg1"]:
@@ -1303,7 +1337,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 L.append(f"  d{a} = {vfma(sv, f'x{b}', f'd{a}')}; d{b} = {vfma(sv, f'x{a}', f'd{b}')};")
             else:
                 carry = [pv, sv]
-        L.append("  " + pin(bv + carry, sgprs=[f"c{t}" for t in nxt]))
+        L.append("  " + pin(bv + carry, sgprs=nxt))
     L.append("  __syncthreads();")
     for a in range(D):
         L.append(f"  {lds_put('xr', lq(lin, a, 'cl'), f'd{a}')}")
@@ -1483,6 +1517,11 @@ def main(outdir: str) -> None:
              "typedef float eelg_f2u __attribute__((ext_vector_type(2), aligned(4)));",
              "typedef float eelg_f4a __attribute__((ext_vector_type(4)));",
              "typedef float eelg_f4r __attribute__((ext_vector_type(4)));",
+             "// SGPR coefficient vectors of the contraction (dword-aligned scalar loads)",
+             "typedef float eelg_c2 __attribute__((ext_vector_type(2), aligned(4)));",
+             "typedef float eelg_c4 __attribute__((ext_vector_type(4), aligned(4)));",
+             "typedef float eelg_c8 __attribute__((ext_vector_type(8), aligned(4)));",
+             "typedef float eelg_c16 __attribute__((ext_vector_type(16), aligned(4)));",
              "typedef float eelg_f2 __attribute__((ext_vector_type(2)));   // a lane's node pair (packed f32 VALU)",
              "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
     for lmax in kernel_sets.LMAX:
