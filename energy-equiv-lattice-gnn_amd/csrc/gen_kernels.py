@@ -62,23 +62,20 @@ SC_BLOCK_BWD = int(os.environ.get("EELG_SC_BLOCK_BWD", "64"))
 # fwd / grad-x: 64-node tiles per workgroup; waves w, w + 4, ... run the same channel on
 # consecutive tiles, so their coefficient scalar loads share the CU's scalar cache
 SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
-# fwd / grad-x: two nodes per lane (rows lane and lane + 64 of a 128-node tile) on packed f32
-# VALU (v_pk_fma_f32 / v_pk_mul_f32, the coefficient broadcast from its SGPR): twice the FMAs
-# per issued instruction and per coefficient load (tools/proto/pkfma_bench.hip, r04c: v_fma_f32
-# 41 / 60 / 67 TFLOP/s at 1 / 2 / 4 waves per SIMD, v_pk_fma_f32 81 / 116 / 130)
-SC_PK = int(os.environ.get("EELG_SC_PK", "0"))
 # fwd / grad-x: a block's coefficients are scalar-loaded as SGPR vectors (16 / 8 / 4 / 2 / 1
 # terms per s_load) and pinned as whole vectors, so the VALU reads them in place; 0 = one float
-# (and one pinned SGPR, hence an s_mov_b32 per term) per coefficient
+# (and one pinned SGPR, hence an s_mov_b32 per term) per coefficient.  r04f kbench: fwd 0.312 vs
+# 0.326 ms, grad-x 0.349 vs 0.357
 SC_CVEC = int(os.environ.get("EELG_SC_CVEC", "1"))
-# waves per SIMD asked of the packed forward / grad-x (amdgpu_waves_per_eu; 0 = the compiler's choice)
-SC_PK_WPE_FWD = int(os.environ.get("EELG_SC_PK_WPE_FWD", "0"))
-SC_PK_WPE_BWD = int(os.environ.get("EELG_SC_PK_WPE_BWD", "0"))
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, the most
 # accumulators (terms) per wave
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
 SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
 SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
+# coefficient gradient: two nodes per lane (adjacent LDS columns read by ds_read_b64) on packed
+# f32 VALU (v_pk_fma_f32: twice the FMAs per issued instruction), the pair's halves added
+# before the lane reduction
+SC_COEF_PK = int(os.environ.get("EELG_SC_COEF_PK", "0"))
 # coefficient gradient: term groups clustered by shared operands (coef_groups) instead of runs
 # of the term order
 SC_COEF_CLUSTER = int(os.environ.get("EELG_SC_COEF_CLUSTER", "1"))
@@ -1076,17 +1073,16 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    PK = bool(SC_PK)
-    NB = 128 if PK else 64 * SC_NT          # nodes per workgroup (fwd / grad-x): one or two per lane
-    NTH = 256 if PK else 256 * SC_NT        # threads per workgroup (fwd / grad-x)
-    VT = "eelg_f2" if PK else "float"       # a lane's value type: its node pair or its node
+    NB = 64 * SC_NT                         # nodes per workgroup (fwd / grad-x), one per lane
+    NTH = 256 * SC_NT                       # threads per workgroup (fwd / grad-x)
+    VT = "float"
 
     def vfma(a, b, c):
-        return f"__builtin_elementwise_fma({a}, {b}, {c})" if PK else f"fmaf({a}, {b}, {c})"
+        return f"fmaf({a}, {b}, {c})"
 
     def cfma(t, b, c):
-        """c += coefficient t * b (the coefficient is a wave-uniform SGPR, broadcast)"""
-        return vfma(f"(eelg_f2)({CE[t]})", b, c) if PK else vfma(CE[t], b, c)
+        """c += coefficient t * b (the coefficient is a wave-uniform SGPR)"""
+        return vfma(CE[t], b, c)
     CE: Dict[int, str] = {}                 # term -> expression of its (SGPR) coefficient
 
     def cload(blk):
@@ -1113,13 +1109,13 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             names.append(nm)
             t += sz
         return out, names
-    zero = "(eelg_f2)(0.0f)" if PK else "0.0f"
+    zero = "0.0f"
 
     def lds_get(ptr, col):
-        return f"(eelg_f2){{{ptr}[{col}], {ptr}[64 * {TP} + {col}]}}" if PK else f"{ptr}[{col}]"
+        return f"{ptr}[{col}]"
 
     def lds_put(ptr, col, v):
-        return f"{ptr}[{col}] = {v}.x; {ptr}[64 * {TP} + {col}] = {v}.y;" if PK else f"{ptr}[{col}] = {v};"
+        return f"{ptr}[{col}] = {v};"
 
     # Staging between the mul-major rows and the quad tile.  A quad owns, per node and l-block,
     # one run of 4*d floats (d float4, 16-B aligned), so a tile of nb nodes is nb * D float4:
@@ -1218,7 +1214,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 f"  const int cq = rest_ % {NQ};",
                 f"  const int n0 = ((rest_ / {NQ}) * 8 + xcd) * {nb};",
                 "  if (n0 >= n_nodes) return;   // uniform per workgroup (tile count padded to 8)"]
-    nrow = "lane" if SC_NT == 1 or PK else "((wv >> 2) * 64 + lane)"   # this lane's (first) node row in the tile
+    nrow = "lane" if SC_NT == 1 else "((wv >> 2) * 64 + lane)"   # this lane's node row in the tile
     head = tile_map(NB) + [
             "  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;",
             f"  const int c = __builtin_amdgcn_readfirstlane(cq * {Q} + (wv & {Q - 1}));",
@@ -1226,8 +1222,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             f"  const float* __restrict__ cf = coef + (size_t)c * {cld};"]
 
     # ---------------- forward ----------------
-    wpe = (lambda w: f" __attribute__((amdgpu_waves_per_eu({w})))" if PK and w else "")
-    L.append(f"__global__ __launch_bounds__({NTH}){wpe(SC_PK_WPE_FWD)} void sc_fwd_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
     L.append("    float* __restrict__ out) {")
     L.append(f"  __shared__ float tile[{NB} * {TP}];")
@@ -1279,7 +1274,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 
 
     # ---------------- backward w.r.t. x ----------------
-    L.append(f"__global__ __launch_bounds__({NTH}){wpe(SC_PK_WPE_BWD)} void sc_bwd_x_{name}(")
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
     L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
     L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
     L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
@@ -1382,8 +1377,13 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
     # lane j of group g ends with the sum of term perm[g * 64 + j] (-1: no term)
     perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
-    nsub = NCB // 64
+
+    def cf(a, b, c):
+        return f"__builtin_elementwise_fma({a}, {b}, {c})" if CPK else f"fmaf({a}, {b}, {c})"
+    CPK = bool(SC_COEF_PK)
+    nsub = NCB // (128 if CPK else 64)
     NC4 = NCB // 4
+    CT = "eelg_f2" if CPK else "float"
     L.append(f"// coefficient gradient: {sum(1 for g in groups if g)} term groups of <= {JG} terms, {gpw} per wave;")
     L.append(f"// one workgroup = one channel x {NCB} LDS-resident nodes")
     L.append(f"__device__ const short sc_coef_perm_{name}[{len(perm)}] = {{")
@@ -1440,9 +1440,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {cld};")
     L.append(f"  for (int k = 0; k < {gpw}; ++k) {{")
     L.append(f"    const int jg = __builtin_amdgcn_readfirstlane(k * {WV} + wv);")
-    L.append("    float acc[64];")
+    L.append(f"    {CT} acc[64];")
     L.append("#pragma unroll")
-    L.append("    for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
+    L.append(f"    for (int i = 0; i < 64; ++i) acc[i] = ({CT})(0.0f);")
     L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
         if not grp:
@@ -1460,11 +1460,18 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         L.append("#pragma unroll 1")
         L.append(f"      for (int sb = 0; sb < {nsub}; ++sb) {{")
-        L.append("        const int o = sb * 64 + lane;")
-        for a in sorted(need_x):
-            L.append(f"        const float x{a} = sx[{a * SXS} + o];")
-        for q in sorted(need_g):
-            L.append(f"        const float g{q} = sg[{q * SXS} + o];")
+        if CPK:
+            L.append("        const int o = sb * 128 + 2 * lane;")
+            for a in sorted(need_x):
+                L.append(f"        const eelg_f2 x{a} = *reinterpret_cast<const eelg_f2*>(sx + {a * SXS} + o);")
+            for q in sorted(need_g):
+                L.append(f"        const eelg_f2 g{q} = *reinterpret_cast<const eelg_f2*>(sg + {q * SXS} + o);")
+        else:
+            L.append("        const int o = sb * 64 + lane;")
+            for a in sorted(need_x):
+                L.append(f"        const float x{a} = sx[{a * SXS} + o];")
+            for q in sorted(need_g):
+                L.append(f"        const float g{q} = sg[{q * SXS} + o];")
         # accumulator jj belongs to term grp[jj]; walk the terms by (a, b, c) so each pair
         # product and each triple product is formed once per group
         order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
@@ -1473,21 +1480,21 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             t = grp[jj]
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
-                L.append(f"        acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
+                L.append(f"        acc[{jj}] = {cf(f'x{a}', f'g{q}', f'acc[{jj}]')};")
                 continue
             if cur != (a, b):
                 if cur is not None:
                     L.append("        }")
                     L.append("        " + cpin)
-                L.append(f"        {{ const float p = x{a} * x{b};")
+                L.append(f"        {{ const {CT} p = x{a} * x{b};")
                 cur, curc = (a, b), None
             if nu == 2:
-                L.append(f"          acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
+                L.append(f"          acc[{jj}] = {cf('p', f'g{q}', f'acc[{jj}]')};")
             else:
                 if curc != cc:
-                    L.append(f"          const float m{cc} = p * x{cc};")
+                    L.append(f"          const {CT} m{cc} = p * x{cc};")
                     curc = cc
-                L.append(f"          acc[{jj}] = fmaf(m{cc}, g{q}, acc[{jj}]);")
+                L.append(f"          acc[{jj}] = {cf(f'm{cc}', f'g{q}', f'acc[{jj}]')};")
         if cur is not None:
             L.append("        }")
         L.append("        " + cpin)
@@ -1495,9 +1502,17 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append("      break; }")
     L.append("    default: break;")
     L.append("    }")
-    L.append("    eelg_lane_reduce64(acc);")
+    if CPK:
+        L.append("    float accs[64];")
+        L.append("#pragma unroll")
+        L.append("    for (int i = 0; i < 64; ++i) accs[i] = acc[i].x + acc[i].y;")
+        L.append("    eelg_lane_reduce64(accs);")
+        L.append("    const float r0 = accs[0];")
+    else:
+        L.append("    eelg_lane_reduce64(acc);")
+        L.append("    const float r0 = acc[0];")
     L.append(f"    const int t = jg < {len(groups)} ? sc_coef_perm_{name}[jg * 64 + lane] : -1;")
-    L.append("    if (t >= 0) dst[t] = acc[0];")
+    L.append("    if (t >= 0) dst[t] = r0;")
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
@@ -1522,8 +1537,8 @@ def main(outdir: str) -> None:
              "typedef float eelg_c4 __attribute__((ext_vector_type(4), aligned(4)));",
              "typedef float eelg_c8 __attribute__((ext_vector_type(8), aligned(4)));",
              "typedef float eelg_c16 __attribute__((ext_vector_type(16), aligned(4)));",
-             "typedef float eelg_f2 __attribute__((ext_vector_type(2)));   // a lane's node pair (packed f32 VALU)",
-             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
+             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));",
+             "typedef float eelg_f2 __attribute__((ext_vector_type(2)));   // a lane's node pair (packed f32 VALU)", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     # the row a tp_fwd stream reads for an edge past its range (also when the batch has no
