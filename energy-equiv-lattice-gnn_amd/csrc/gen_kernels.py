@@ -72,10 +72,6 @@ SC_CVEC = int(os.environ.get("EELG_SC_CVEC", "1"))
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
 SC_COEF_WAVES = int(os.environ.get("EELG_SC_COEF_WAVES", "16"))
 SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
-# coefficient gradient: two nodes per lane (adjacent LDS columns read by ds_read_b64) on packed
-# f32 VALU (v_pk_fma_f32: twice the FMAs per issued instruction), the pair's halves added
-# before the lane reduction
-SC_COEF_PK = int(os.environ.get("EELG_SC_COEF_PK", "0"))
 # coefficient gradient: term groups clustered by shared operands (coef_groups) instead of runs
 # of the term order
 SC_COEF_CLUSTER = int(os.environ.get("EELG_SC_COEF_CLUSTER", "1"))
@@ -1377,13 +1373,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         groups = [list(range(s, min(s + JG, nt))) for s in range(0, nt, JG)]
     # lane j of group g ends with the sum of term perm[g * 64 + j] (-1: no term)
     perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
-
-    def cf(a, b, c):
-        return f"__builtin_elementwise_fma({a}, {b}, {c})" if CPK else f"fmaf({a}, {b}, {c})"
-    CPK = bool(SC_COEF_PK)
-    nsub = NCB // (128 if CPK else 64)
+    nsub = NCB // 64
     NC4 = NCB // 4
-    CT = "eelg_f2" if CPK else "float"
     L.append(f"// coefficient gradient: {sum(1 for g in groups if g)} term groups of <= {JG} terms, {gpw} per wave;")
     L.append(f"// one workgroup = one channel x {NCB} LDS-resident nodes")
     L.append(f"__device__ const short sc_coef_perm_{name}[{len(perm)}] = {{")
@@ -1440,9 +1431,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append(f"  float* __restrict__ dst = part + ((size_t)ch * {MUL} + c) * {cld};")
     L.append(f"  for (int k = 0; k < {gpw}; ++k) {{")
     L.append(f"    const int jg = __builtin_amdgcn_readfirstlane(k * {WV} + wv);")
-    L.append(f"    {CT} acc[64];")
+    L.append("    float acc[64];")
     L.append("#pragma unroll")
-    L.append(f"    for (int i = 0; i < 64; ++i) acc[i] = ({CT})(0.0f);")
+    L.append("    for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
     L.append("    switch (jg) {")
     for gi, grp in enumerate(groups):
         if not grp:
@@ -1460,18 +1451,11 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         L.append("#pragma unroll 1")
         L.append(f"      for (int sb = 0; sb < {nsub}; ++sb) {{")
-        if CPK:
-            L.append("        const int o = sb * 128 + 2 * lane;")
-            for a in sorted(need_x):
-                L.append(f"        const eelg_f2 x{a} = *reinterpret_cast<const eelg_f2*>(sx + {a * SXS} + o);")
-            for q in sorted(need_g):
-                L.append(f"        const eelg_f2 g{q} = *reinterpret_cast<const eelg_f2*>(sg + {q * SXS} + o);")
-        else:
-            L.append("        const int o = sb * 64 + lane;")
-            for a in sorted(need_x):
-                L.append(f"        const float x{a} = sx[{a * SXS} + o];")
-            for q in sorted(need_g):
-                L.append(f"        const float g{q} = sg[{q * SXS} + o];")
+        L.append("        const int o = sb * 64 + lane;")
+        for a in sorted(need_x):
+            L.append(f"        const float x{a} = sx[{a * SXS} + o];")
+        for q in sorted(need_g):
+            L.append(f"        const float g{q} = sg[{q * SXS} + o];")
         # accumulator jj belongs to term grp[jj]; walk the terms by (a, b, c) so each pair
         # product and each triple product is formed once per group
         order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
@@ -1480,21 +1464,21 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             t = grp[jj]
             nu, (a, b, cc), q = plan.terms[t]
             if nu == 1:
-                L.append(f"        acc[{jj}] = {cf(f'x{a}', f'g{q}', f'acc[{jj}]')};")
+                L.append(f"        acc[{jj}] = fmaf(x{a}, g{q}, acc[{jj}]);")
                 continue
             if cur != (a, b):
                 if cur is not None:
                     L.append("        }")
                     L.append("        " + cpin)
-                L.append(f"        {{ const {CT} p = x{a} * x{b};")
+                L.append(f"        {{ const float p = x{a} * x{b};")
                 cur, curc = (a, b), None
             if nu == 2:
-                L.append(f"          acc[{jj}] = {cf('p', f'g{q}', f'acc[{jj}]')};")
+                L.append(f"          acc[{jj}] = fmaf(p, g{q}, acc[{jj}]);")
             else:
                 if curc != cc:
-                    L.append(f"          const {CT} m{cc} = p * x{cc};")
+                    L.append(f"          const float m{cc} = p * x{cc};")
                     curc = cc
-                L.append(f"          acc[{jj}] = {cf(f'm{cc}', f'g{q}', f'acc[{jj}]')};")
+                L.append(f"          acc[{jj}] = fmaf(m{cc}, g{q}, acc[{jj}]);")
         if cur is not None:
             L.append("        }")
         L.append("        " + cpin)
@@ -1502,17 +1486,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         L.append("      break; }")
     L.append("    default: break;")
     L.append("    }")
-    if CPK:
-        L.append("    float accs[64];")
-        L.append("#pragma unroll")
-        L.append("    for (int i = 0; i < 64; ++i) accs[i] = acc[i].x + acc[i].y;")
-        L.append("    eelg_lane_reduce64(accs);")
-        L.append("    const float r0 = accs[0];")
-    else:
-        L.append("    eelg_lane_reduce64(acc);")
-        L.append("    const float r0 = acc[0];")
+    L.append("    eelg_lane_reduce64(acc);")
     L.append(f"    const int t = jg < {len(groups)} ? sc_coef_perm_{name}[jg * 64 + lane] : -1;")
-    L.append("    if (t >= 0) dst[t] = r0;")
+    L.append("    if (t >= 0) dst[t] = acc[0];")
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
@@ -1537,8 +1513,7 @@ def main(outdir: str) -> None:
              "typedef float eelg_c4 __attribute__((ext_vector_type(4), aligned(4)));",
              "typedef float eelg_c8 __attribute__((ext_vector_type(8), aligned(4)));",
              "typedef float eelg_c16 __attribute__((ext_vector_type(16), aligned(4)));",
-             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));",
-             "typedef float eelg_f2 __attribute__((ext_vector_type(2)));   // a lane's node pair (packed f32 VALU)", ""]
+             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     # the row a tp_fwd stream reads for an edge past its range (also when the batch has no
