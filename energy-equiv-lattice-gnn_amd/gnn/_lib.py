@@ -59,6 +59,9 @@ _SIGS = {
     "eelg_linear_pack": ([_P, _P, _P, _P], _I),
     "eelg_linear_fwd_pk": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_split_bf16x3": ([_P, ctypes.c_longlong, _P, _P], _I),
+    "eelg_sum_rows_work": ([_I, ctypes.c_longlong], ctypes.c_longlong),
+    "eelg_sum_rows": ([_P, ctypes.c_longlong, _I, ctypes.c_longlong, ctypes.c_float, _P, _P,
+                       ctypes.c_longlong, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
 }

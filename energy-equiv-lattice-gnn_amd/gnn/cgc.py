@@ -68,7 +68,7 @@ class _CGCConv(torch.autograd.Function):
         gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)   # per-sender sums of dz
         ws, wr, we = w[:, :d], w[:, d: 2 * d], w[:, 2 * d:]
         dw = torch.cat([ops._wgrad(gs, x), ops._wgrad(gr, x), ops._wgrad(dz, edge_ft)], dim=1)
-        db = gr.sum(0)
+        db = ops.sum_rows(gr)
         dx = gs @ ws + gr @ wr
         dedge = dz @ we
         return dx, dedge, dw[:d], db[:d], dw[d:], db[d:], None, None

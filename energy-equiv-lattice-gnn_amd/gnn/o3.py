@@ -332,7 +332,7 @@ class Linear(torch.nn.Module):
         return gx
 
     def _bwd_w(self, x, gy):
-        from . import _lib
+        from . import _lib, ops
         n = x.shape[0]
         if not self.instructions:
             return torch.zeros_like(self.weight)
@@ -347,12 +347,18 @@ class Linear(torch.nn.Module):
             _lib.ptr(x), self.irreps_in.dim, _lib.ptr(gy), self.irreps_out.dim, n, nps,
             _lib.ptr(part), slices, self.weight_numel, ctypes.byref(self._bw_desc), _lib.stream(part)),
             "linear_bwd_w")
-        return part.sum(0)
+        return ops.sum_rows(part)
 
     def _bwd_bias(self, gy):
-        parts = [gy[:, self._out_off[o]: self._out_off[o] + self.irreps_out[o].mul].sum(0)
-                 for o in self.bias_slots]
-        return torch.cat(parts)
+        from . import ops
+        out = torch.empty(sum(self.irreps_out[o].mul for o in self.bias_slots), device=gy.device,
+                          dtype=torch.float32)
+        k = 0
+        for o in self.bias_slots:
+            m = self.irreps_out[o].mul
+            ops.sum_rows(gy[:, self._out_off[o]: self._out_off[o] + m], out=out[k: k + m])
+            k += m
+        return out
 
     def forward(self, x: torch.Tensor, residual: torch.Tensor = None,
                 grad_mailbox: "GradMailbox" = None) -> torch.Tensor:

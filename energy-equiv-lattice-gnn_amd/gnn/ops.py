@@ -6,6 +6,7 @@ There is no eager/CPU fallback: a missing library or a CPU tensor raises.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -490,7 +491,7 @@ class _SymCon(torch.autograd.Function):
                 _lib.check(lib.eelg_sc_bwd_coef(ctx.cfg, _lib.ptr(xt), _lib.ptr(gt), n, ctx.mul,
                                                 chunk, _lib.ptr(part), _lib.stream(part)), "sc_bwd_coef")
                 TIMER.stop(tok)
-                gcoef = part.sum(0)
+                gcoef = sum_rows(part)
         return gx, gcoef, None, None, None, None
 
 
@@ -522,8 +523,8 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, chunk: int = 512) -> torch.Tensor:
     out = None
     if c > 1:
         m = c * chunk
-        out = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2),
-                        x[:m].view(c, chunk, -1)).sum(0, dtype=acc)
+        prod = torch.bmm(g[:m].view(c, chunk, -1).transpose(1, 2), x[:m].view(c, chunk, -1))
+        out = sum_rows(prod) if prod.dtype == torch.float32 else prod.sum(0, dtype=acc)
         g, x = g[m:], x[m:]
     if g.shape[0]:
         rest = (g.t() @ x).to(acc)
@@ -541,6 +542,31 @@ def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
     _lib.check(_lib.load().eelg_split_bf16x3(_lib.ptr(t), t.numel(), _lib.ptr(parts),
                                              _lib.stream(parts)), "split_bf16x3")
     return parts
+
+
+def sum_rows(part: torch.Tensor, out: torch.Tensor = None, scale: float = 1.0) -> torch.Tensor:
+    """``scale * part.sum(0)`` on the device in a fixed order (``eelg_sum_rows``): ``part`` is
+    [rows, ...] with contiguous trailing dims, or a 2-D view whose rows are strided (a column
+    block of a wider tensor: the bias gradient of one output slot).  ``out`` (contiguous,
+    ``part.shape[1:]``) receives the sum when given."""
+    _require_device(part)
+    if part.dtype != torch.float32:
+        raise TypeError(f"sum_rows: float32 expected, got {part.dtype}")
+    rows = part.shape[0]
+    if part.dim() == 2 and part.stride(1) == 1:
+        ld, cols = part.stride(0), part.shape[1]
+    else:
+        part = part.contiguous()
+        cols = math.prod(part.shape[1:])
+        ld = cols
+    if out is None:
+        out = torch.empty(part.shape[1:], device=part.device, dtype=torch.float32)
+    lib = _lib.load()
+    nw = lib.eelg_sum_rows_work(rows, cols)
+    work = torch.empty(nw, device=part.device, dtype=torch.float32) if nw else None
+    _lib.check(lib.eelg_sum_rows(_lib.ptr(part), max(ld, cols), rows, cols, float(scale), _lib.ptr(out),
+                                 _lib.ptr(work), nw, _lib.stream(out)), "sum_rows")
+    return out
 
 
 def _radial_desc(params, n_feat: int):
@@ -644,7 +670,7 @@ class _RadialMLP(torch.autograd.Function):
                                            ctypes.byref(d), _lib.ptr(wot_parts), _lib.ptr(z),
                                            _lib.ptr(feats[a:b]), _lib.ptr(grad_h), _lib.ptr(part_h),
                                            _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd")
-            sm, wo = part_h.sum(0), part_wo.sum(0)
+            sm, wo = sum_rows(part_h), sum_rows(part_wo)
             small = sm if small is None else small + sm
             gwo = wo if gwo is None else gwo + wo
         grads, off = [], 0

@@ -296,6 +296,17 @@ int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_r
                     const void* wot_parts, const float* zsave, const float* feats, float* grad_h,
                     float* part_h, float* part_wo, void* stream);
 
+/* Deterministic sum over the leading dimension of partial results (the partial buffers of
+ * eelg_linear_bwd_w, eelg_radial_bwd and eelg_sc_bwd_coef, and the bias gradients = column
+ * sums of grad_out; replaces the reference's implicit autograd reductions, gnn/blocks.py and
+ * e3nn o3.Linear biases): out[c] = scale * sum_{r < rows} part[r*ld + c] for c < cols, rows
+ * summed in a fixed order.  rows > 2048 needs a workspace of eelg_sum_rows_work(rows, cols)
+ * floats (0 otherwise).  16-byte aligned part / out with ld, cols multiples of 4 take the
+ * float4 path.  -2 on bad sizes. */
+long long eelg_sum_rows_work(int rows, long long cols);
+int eelg_sum_rows(const float* part, long long ld, int rows, long long cols, float scale, float* out,
+                  float* work, long long work_len, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,11 +90,14 @@ def _near_tie_senders(msg, edge_index, reduce, rtol):
         if sel.numel() < 2:
             continue
         v = sgn * msg[sel]
-        best = v.min(0).values
-        close = (v - best) <= rtol * scale                 # [k, C]: the pick and any near-tie
-        multi = close.sum(0) > 1
-        if multi.any():
-            rows = close[:, multi].any(1).nonzero().flatten()
+        gap = v - v.min(0).values                          # [k, C]; 0 at the pick
+        # a runner-up strictly above the pick but within rtol: exact ties (equal fp64 values,
+        # e.g. components that vanish on several edges) are decided by the same first-index
+        # rule on both sides and stay compared
+        near = (gap > 0) & (gap <= rtol * scale)
+        cols = near.any(0)
+        if cols.any():
+            rows = ((gap[:, cols] <= rtol * scale).any(1)).nonzero().flatten()
             tied |= {int(send[sel[r]]) for r in rows}
     return tied
 
