@@ -773,7 +773,10 @@ static bool lin_fwd_fast_ok(const float* x, int x_row, const float* y, int y_row
 #endif
 #define LINX_KMAX 320   // summed source K of a slot held in LDS (10 chunks x 6 KB)
 
-template <int D, bool RES>
+// ONE: the slot sums a single 32-wide K chunk (K = 32: the grad-x of the 7360 -> 800 linear, the
+// 800 -> 800 linears), so every group of the wave multiplies the same B tile: its 2 x 3
+// fragments stay in registers instead of being re-read from LDS per group
+template <int D, bool RES, bool ONE>
 __device__ __forceinline__ void lin_fwd_x6(const float* __restrict__ x, int x_row,
                                            const float* __restrict__ bias, int n_nodes,
                                            float* __restrict__ y, int y_row,
@@ -814,6 +817,13 @@ __device__ __forceinline__ void lin_fwd_x6(const float* __restrict__ x, int x_ro
   eelg_f32x16v acc;
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = bj;
+  uint4 bone[2][3];
+  if (ONE) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bone[kb][p] = bs[(kb * 3 + p) * 64 + lane];
+  }
   float4 ra[G::NQ];
   load(0, ra);
   for (int q = 0; q < nq; ++q) {
@@ -837,7 +847,7 @@ __device__ __forceinline__ void lin_fwd_x6(const float* __restrict__ x, int x_ro
       uint4 ap[3], bp[3];
       eelg_split8(av, ap);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bp[p] = bs[((c * 2 + kb) * 3 + p) * 64 + lane];
+      for (int p = 0; p < 3; ++p) bp[p] = ONE ? bone[kb][p] : bs[((c * 2 + kb) * 3 + p) * 64 + lane];
       EELG_X6(acc, ap, bp);
     }
     __builtin_amdgcn_wave_barrier();
@@ -933,12 +943,23 @@ __global__ __launch_bounds__(64 * LINX_WAVES) void lin_fwd_x6_kernel(
   __syncthreads();
   float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
   const int g0 = gb * LINX_WAVES * LINX_GPW, g1 = min(n_groups, g0 + LINX_WAVES * LINX_GPW);
+  const bool one = nch == 1;
   switch (d) {
-    case 1: lin_fwd_x6<1, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
-    case 3: lin_fwd_x6<3, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
-    case 5: lin_fwd_x6<5, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
-    case 7: lin_fwd_x6<7, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
-    default: lin_fwd_x6<9, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res); break;
+    case 1: if (one) lin_fwd_x6<1, RES, true>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            else lin_fwd_x6<1, RES, false>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            break;
+    case 3: if (one) lin_fwd_x6<3, RES, true>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            else lin_fwd_x6<3, RES, false>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            break;
+    case 5: if (one) lin_fwd_x6<5, RES, true>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            else lin_fwd_x6<5, RES, false>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            break;
+    case 7: if (one) lin_fwd_x6<7, RES, true>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            else lin_fwd_x6<7, RES, false>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+            break;
+    default: if (one) lin_fwd_x6<9, RES, true>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+             else lin_fwd_x6<9, RES, false>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, bs, xw, res);
+             break;
   }
 }
 
