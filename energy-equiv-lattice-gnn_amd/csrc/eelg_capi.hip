@@ -610,8 +610,13 @@ int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* s
                  const float* grad_agg, float* dz, float* grad_pr, void* stream) {
   if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
   if (n_nodes <= 0) return 0;
-  hipLaunchKernelGGL(cgc_bwd_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                     pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
+  if (D > 128) return fail(-2, "cgc_bwd: D = %d > 128 not built", D);
+  if (D > 64)
+    hipLaunchKernelGGL(cgc_bwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
+  else
+    hipLaunchKernelGGL(cgc_bwd_kernel<1>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
   return check_launch("cgc_bwd");
 }
 

@@ -20,7 +20,9 @@ __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + ex
 // wave-uniform (one scalar load batch), and every lane issues the batch's gathers of Ps[s] and
 // Ep[e] before it evaluates any of them, so a receiver costs about three memory round trips
 // instead of two per edge.  A lane owns channels lane + 64 k, k < CPL (CPL = ceil(D / 64)).
+#ifndef CGC_EB
 #define CGC_EB 4
+#endif
 template <int CPL>
 __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
@@ -70,36 +72,68 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
 
 // Backward: per receiver, recompute z_e and write dz_e = d msg / d z_e (.) g_n for every
 // in-edge, and the receiver sums Gr[n] = sum_e dz_e in the same pass.  The sender sums
-// Gs (for dW_s and dx) are a segmented sum of dz over the sender CSR.
+// Gs (for dW_s and dx) are a segmented sum of dz over the sender CSR.  Edges are taken CGC_EB
+// at a time like the forward: the batch's sender indices are read together and every gather
+// of Ps[s] / Ep[e] is issued before any of them is used.
+template <int CPL>
 __global__ __launch_bounds__(256) void cgc_bwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
     const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, const float* __restrict__ gagg, float* __restrict__ dz, float* __restrict__ gr) {
-  const int node = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (node >= n_nodes) return;
   const int beg = rowptr[node], end = rowptr[node + 1];
   const int D2 = 2 * D;
   const float sc = row_scale ? row_scale[node] : 1.0f;
   const float* __restrict__ prn = pr + (size_t)node * D2;
-  for (int c = lane; c < D; c += 64) {
-    const float rv = prn[c], rm = prn[D + c];
-    const float g = gagg[(size_t)node * D + c] * sc;
-    float av = 0.0f, am = 0.0f;
-    for (int e = beg; e < end; ++e) {
-      const int s = sender[e];
-      const float zv = ps[(size_t)s * D2 + c] + rv + ep[(size_t)e * D2 + c];
-      const float zm = ps[(size_t)s * D2 + D + c] + rm + ep[(size_t)e * D2 + D + c];
-      const float sv = zv > 20.0f ? 1.0f : cgc_sigmoid(zv);   // softplus' (torch: 1 above threshold)
-      const float sm = cgc_sigmoid(zm);
-      const float dv = g * sv * sm;
-      const float dm = g * cgc_softplus(zv) * sm * (1.0f - sm);
-      dz[(size_t)e * D2 + c] = dv;
-      dz[(size_t)e * D2 + D + c] = dm;
-      av += dv;
-      am += dm;
-    }
-    gr[(size_t)node * D2 + c] = av;
-    gr[(size_t)node * D2 + D + c] = am;
+  float rv[CPL], rm[CPL], g[CPL], av[CPL], am[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = min(lane + 64 * k, D - 1);
+    rv[k] = prn[c];
+    rm[k] = prn[D + c];
+    g[k] = gagg[(size_t)node * D + c] * sc;
+    av[k] = 0.0f;
+    am[k] = 0.0f;
   }
+  for (int e0 = beg; e0 < end; e0 += CGC_EB) {
+    int s[CGC_EB];
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j) s[j] = sender[min(e0 + j, end - 1)];
+    float zv[CGC_EB][CPL], zm[CGC_EB][CPL];
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j) {
+      const int e = min(e0 + j, end - 1);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int c = min(lane + 64 * k, D - 1);
+        zv[j][k] = ps[(size_t)s[j] * D2 + c] + ep[(size_t)e * D2 + c];
+        zm[j][k] = ps[(size_t)s[j] * D2 + D + c] + ep[(size_t)e * D2 + D + c];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CGC_EB; ++j)
+      if (e0 + j < end)   // uniform
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const float z1 = zv[j][k] + rv[k], z2 = zm[j][k] + rm[k];
+          const float sv = z1 > 20.0f ? 1.0f : cgc_sigmoid(z1);   // softplus' (torch: 1 above threshold)
+          const float sm = cgc_sigmoid(z2);
+          const float dv = g[k] * sv * sm;
+          const float dm = g[k] * cgc_softplus(z1) * sm * (1.0f - sm);
+          if (lane + 64 * k < D) {
+            dz[(size_t)(e0 + j) * D2 + lane + 64 * k] = dv;
+            dz[(size_t)(e0 + j) * D2 + D + lane + 64 * k] = dm;
+          }
+          av[k] += dv;
+          am[k] += dm;
+        }
+  }
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+    if (lane + 64 * k < D) {
+      gr[(size_t)node * D2 + lane + 64 * k] = av[k];
+      gr[(size_t)node * D2 + D + lane + 64 * k] = am[k];
+    }
 }

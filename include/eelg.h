@@ -175,7 +175,7 @@ int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* s
                  const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
                  void* stream);
 /* Backward: dz[E, 2D] = d agg / d z per edge and grad_pr[N, 2D] = receiver sums of dz;
- * the sender sums are eelg_segment_sum_csr(dz, srowptr, sperm). */
+ * the sender sums are eelg_segment_sum_csr(dz, srowptr, sperm).  D <= 128 as the forward. */
 int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D,
                  const float* grad_agg, float* dz, float* grad_pr, void* stream);
