@@ -80,17 +80,35 @@ __device__ __forceinline__ int rad_row(int r, int hf) { return (r & 3) + 8 * (r 
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
+// RAD_FWD_CT: output column tiles per staged W_o block (one barrier per block, CT independent
+// accumulator chains); RAD_FWD_WPE: waves per SIMD asked of the compiler (0 = its choice)
+#ifndef RAD_FWD_CT
+#define RAD_FWD_CT 1
+#endif
+#ifndef RAD_FWD_WPE
+#define RAD_FWD_WPE 0
+#endif
+#if RAD_FWD_WPE > 0
+#define RAD_FWD_ATTR __attribute__((amdgpu_waves_per_eu(RAD_FWD_WPE)))
+#else
+#define RAD_FWD_ATTR
+#endif
 template <int H, int NH, bool BF>
-__global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict__ feats,
+__global__ __launch_bounds__(256) RAD_FWD_ATTR void radial_fwd_kernel(const float* __restrict__ feats,
                                                          int n_edges, eelg_radial_desc d,
                                                          const unsigned short* __restrict__ wop,
                                                          float* __restrict__ zsave,
                                                          void* __restrict__ out) {
   constexpr int HS = H + 1, NT = H / 32, KH = H / 2, ES = BF ? 2 : 4, NKB = H / 16;
-  constexpr int NBF = 3 * NKB * 64;           // B fragments (uint4) of one 32-column tile, all parts
+  constexpr int CT = RAD_FWD_CT;
+  constexpr int NBF = 3 * NKB * 64 * CT;      // B fragments (uint4) of CT 32-column tiles, all parts
   constexpr int BPT = (NBF + 255) / 256;
-  __shared__ float hb[4 * 32 * HS];
-  __shared__ uint4 bt[2][NBF];                // [buf][((part * NKB + kb) * 2 + hf) * 32 + col]
+  // the hidden activations (hb) and, once every wave has its A fragments, the double-buffered
+  // W_o blocks (bt: [buf][tile][((part * NKB + kb) * 2 + hf) * 32 + col]) share one LDS region
+  constexpr int HB_BYTES = 4 * 32 * HS * 4, BT_BYTES = 2 * NBF * 16;
+  __shared__ uint4 smem[(HB_BYTES > BT_BYTES ? HB_BYTES : BT_BYTES) / 16];
+  float* __restrict__ hb = reinterpret_cast<float*>(smem);
+  uint4 (*bt)[NBF] = reinterpret_cast<uint4 (*)[NBF]>(smem);
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
   const int e0 = (blockIdx.x * 4 + wave) * 32;
   const int F = d.n_feat, W = d.n_out;
@@ -163,12 +181,13 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
   }
   const int nct = (W + 31) >> 5;
   uint4 rb[BPT];
-  auto load_b = [&](int ct) {
+  auto load_b = [&](int ct) {   // tiles ct .. ct + CT - 1
 #pragma unroll
     for (int q = 0; q < BPT; ++q) {
       const int idx = threadIdx.x + 256 * q;
-      const int p = idx / (NKB * 64), rem = idx - p * (NKB * 64);
-      const int kb = rem >> 6, h2 = (rem >> 5) & 1, col = ct * 32 + (rem & 31);
+      const int tt = idx / (3 * NKB * 64), r0 = idx - tt * (3 * NKB * 64);
+      const int p = r0 / (NKB * 64), rem = r0 - p * (NKB * 64);
+      const int kb = rem >> 6, h2 = (rem >> 5) & 1, col = (ct + tt) * 32 + (rem & 31);
       rb[q] = (idx < NBF && col < W)
                   ? *reinterpret_cast<const uint4*>(wop + ((size_t)p * W + col) * H + 16 * kb + 8 * h2)
                   : make_uint4(0u, 0u, 0u, 0u);
@@ -182,31 +201,39 @@ __global__ __launch_bounds__(256) void radial_fwd_kernel(const float* __restrict
     }
   };
   load_b(0);
+  __syncthreads();   // every wave has read its hidden activations: the region becomes bt
   store_b(0);
   __syncthreads();
-  for (int ct = 0; ct < nct; ++ct) {
-    if (ct + 1 < nct) load_b(ct + 1);
-    const uint4* __restrict__ bb = bt[ct & 1] + hf * 32 + i;
-    rad_f32x16 acc;
+  for (int c0 = 0, buf = 0; c0 < nct; c0 += CT, buf ^= 1) {
+    if (c0 + CT < nct) load_b(c0 + CT);
+    rad_f32x16 acc[CT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    for (int tt = 0; tt < CT; ++tt)
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
-      uint4 b[3];
+      for (int r = 0; r < 16; ++r) acc[tt][r] = 0.0f;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b[p] = bb[(p * NKB + kb) * 64];
-      EELG_X6(acc, ap[kb], b);
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int tt = 0; tt < CT; ++tt) {
+        const uint4* __restrict__ bb = bt[buf] + tt * 3 * NKB * 64 + hf * 32 + i;
+        uint4 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = bb[(p * NKB + kb) * 64];
+        EELG_X6(acc[tt], ap[kb], b);
+      }
+#pragma unroll
+    for (int tt = 0; tt < CT; ++tt) {
+      const int col = (c0 + tt) * 32 + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t off = rad_off(((uint32_t)(e0 + rad_row(r, hf)) * W + col) * ES, col < W);
+        if (BF)
+          rad_bst16(ro, off, eelg_f2bf(acc[tt][r]));
+        else
+          rad_bst(ro, off, acc[tt][r]);
+      }
     }
-    const int col = ct * 32 + i;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t off = rad_off(((uint32_t)(e0 + rad_row(r, hf)) * W + col) * ES, col < W);
-      if (BF)
-        rad_bst16(ro, off, eelg_f2bf(acc[r]));
-      else
-        rad_bst(ro, off, acc[r]);
-    }
-    if (ct + 1 < nct) store_b((ct + 1) & 1);
+    if (c0 + CT < nct) store_b(buf ^ 1);
     __syncthreads();
   }
 }
