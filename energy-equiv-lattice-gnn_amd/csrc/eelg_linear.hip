@@ -540,6 +540,17 @@ __device__ __forceinline__ void lin_stage_w(const float* __restrict__ w, const e
   }
 }
 
+// LINF_NT: the fast kernel's output stores nontemporal (streaming past L2; experiment knob)
+#ifndef LINF_NT
+#define LINF_NT 0
+#endif
+#if LINF_NT
+typedef float linf_f4n __attribute__((ext_vector_type(4)));
+#define LINF_STORE(v, p) \
+  __builtin_nontemporal_store(__builtin_bit_cast(linf_f4n, (v)), reinterpret_cast<linf_f4n*>(p))
+#else
+#define LINF_STORE(v, p) (*(p) = (v))
+#endif
 template <int D, bool RES>
 __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
                                              const float* __restrict__ bias, int n_nodes,
@@ -641,7 +652,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
           const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
           float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
           if (RES) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
-          *reinterpret_cast<float4*>(yb + o) = v;
+          LINF_STORE(v, reinterpret_cast<float4*>(yb + o));
         }
       }
       __builtin_amdgcn_wave_barrier();
