@@ -56,6 +56,12 @@ __device__ __forceinline__ void rad_bst(rad_rsrc_t r, uint32_t off, float v) {
 __device__ __forceinline__ void rad_bst16(rad_rsrc_t r, uint32_t off, unsigned short v) {
   __builtin_amdgcn_raw_buffer_store_b16(v, r, (int)off, 0, 0);
 }
+// RAD_FWD_NT: the forward's w stores nontemporal (cache policy nt: w is read by tp_fwd layers
+// later, after the other layers' MLPs have streamed through the caches)
+#ifndef RAD_FWD_NT
+#define RAD_FWD_NT 0
+#endif
+#define RAD_W_POLICY (RAD_FWD_NT ? 2 : 0)
 // a masked lane's offset gets bit 31 (past every buffer): arithmetic, so the compiler keeps
 // one unconditional buffer access instead of branching around two
 __device__ __forceinline__ uint32_t rad_off(uint32_t off, bool ok) {
@@ -228,9 +234,9 @@ __global__ __launch_bounds__(256) RAD_FWD_ATTR void radial_fwd_kernel(const floa
       for (int r = 0; r < 16; ++r) {
         const uint32_t off = rad_off(((uint32_t)(e0 + rad_row(r, hf)) * W + col) * ES, col < W);
         if (BF)
-          rad_bst16(ro, off, eelg_f2bf(acc[tt][r]));
+          __builtin_amdgcn_raw_buffer_store_b16(eelg_f2bf(acc[tt][r]), ro, (int)off, 0, RAD_W_POLICY);
         else
-          rad_bst(ro, off, acc[tt][r]);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[tt][r]), ro, (int)off, 0, RAD_W_POLICY);
       }
     }
     if (c0 + CT < nct) store_b(buf ^ 1);

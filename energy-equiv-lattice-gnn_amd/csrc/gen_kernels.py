@@ -51,6 +51,9 @@ TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
 TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
+# tp_bwd (fp32): grad_w and gxe stored nontemporal (read back by later kernels: the sender sum,
+# the radial MLP backward on its side stream)
+TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "0"))
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
@@ -243,13 +246,17 @@ def vec_load(names: Sequence[str], base: str, start: str) -> List[str]:
     return out
 
 
-def vec_store(vals: Sequence[str], base: str, start: str) -> List[str]:
-    """base[start + i] = vals[i] with dword-aligned 4/3/2-wide stores"""
+def vec_store(vals: Sequence[str], base: str, start: str, nt: bool = False) -> List[str]:
+    """base[start + i] = vals[i] with dword-aligned 4/3/2-wide stores (nontemporal when nt)"""
     out, i = [], 0
     while i < len(vals):
         w = min(4, len(vals) - i)
         if w == 1:
-            out.append(f"{base}[{start} + {i}] = {vals[i]};")
+            out.append(f"__builtin_nontemporal_store({vals[i]}, &{base}[{start} + {i}]);" if nt
+                       else f"{base}[{start} + {i}] = {vals[i]};")
+        elif nt:
+            out.append(f"__builtin_nontemporal_store({_VT[w]}{{" + ", ".join(vals[i: i + w])
+                       + f"}}, reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}));")
         else:
             out.append(f"*reinterpret_cast<{_VT[w]}*>({base} + {start} + {i}) = {_VT[w]}{{"
                        + ", ".join(vals[i: i + w]) + "};")
@@ -758,7 +765,10 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
                 if ts:
                     gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
             gexpr = " + ".join(gterms) if gterms else "0.0f"
-            L.append(f"        gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
+            if TP_BWD_NT and not bf:
+                L.append(f"        __builtin_nontemporal_store(cp * ({gexpr}), &gwe[{p.slot * MUL}]);")
+            else:
+                L.append(f"        gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
             L.append(f"        const float hw = cp * w{p.slot};")
             for i in range(d1):
                 ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
@@ -769,7 +779,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
         if bf:
             L += [f"      gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
         else:
-            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}")]
+            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}",
+                                                       nt=bool(TP_BWD_NT))]
         if EPH > 1:
             L.append("      " + " ".join(f"{v} = n{v};" for v in xs_ + ys_ + g0_) + " rcur = rn;")
         L.append("    }")
