@@ -59,7 +59,7 @@ __device__ __forceinline__ void rad_bst16(rad_rsrc_t r, uint32_t off, unsigned s
 // RAD_FWD_NT: the forward's w stores nontemporal (cache policy nt: w is read by tp_fwd layers
 // later, after the other layers' MLPs have streamed through the caches)
 #ifndef RAD_FWD_NT
-#define RAD_FWD_NT 0
+#define RAD_FWD_NT 1   // r04r: radial forward 0.254 -> 0.202 ms (kbench), step +0.6 %
 #endif
 #define RAD_W_POLICY (RAD_FWD_NT ? 2 : 0)
 // a masked lane's offset gets bit 31 (past every buffer): arithmetic, so the compiler keeps

@@ -52,8 +52,8 @@ TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
 TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
 # tp_bwd (fp32): grad_w and gxe stored nontemporal (read back by later kernels: the sender sum,
-# the radial MLP backward on its side stream)
-TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "0"))
+# the radial MLP backward on its side stream).  r04r: kbench 0.701 -> 0.683 ms, step +0.3-0.4 %
+TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "1"))
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
