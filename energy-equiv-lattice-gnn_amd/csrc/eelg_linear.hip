@@ -270,20 +270,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
 // (node, m) rows: row r = (n, m) sits at n*32*D + m, and lane u reads x[r][u] at + u*D, an odd
 // stride (D = 2l+1) over the 32 banks, so the operand reads are conflict-free too.  Rows past
 // NB*D point at a zeroed node region.  Same partial layout as the general path.
-// LINW_NTX: grad-W streams its x operand with nontemporal loads (each x element is read by one
-// weight tile; g is re-read by every u-tile of its slice and stays cacheable)
-#ifndef LINW_NTX
-#define LINW_NTX 0
-#endif
-#if LINW_NTX
-typedef float linw_f4n __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 linw_ldx(const float4* p) {
-  return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const linw_f4n*>(p)));
-}
-#define LINW_LOADX(p) linw_ldx(p)
-#else
-#define LINW_LOADX(p) (*(p))
-#endif
 template <int D>
 __device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x_row,
                                               const float* __restrict__ g, int g_row, int n0,
@@ -315,8 +301,7 @@ __device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x
       const int a = f / RUN4, w4 = f - a * RUN4;
       const bool ok = f < NB * RUN4 && nc + a < n1;
       const int nn = ok ? nc + a : 0;
-      rx[q] = ok ? LINW_LOADX(reinterpret_cast<const float4*>(xb + (size_t)nn * x_row + 4 * w4))
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      rx[q] = ok ? *reinterpret_cast<const float4*>(xb + (size_t)nn * x_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
       rg[q] = ok ? *reinterpret_cast<const float4*>(gb + (size_t)nn * g_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
