@@ -47,6 +47,10 @@ TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
 TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
 # LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
 TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
+# LDS-DMA tp_fwd: a group's weight slices lead its chunk list, and the LDS-DMA instructions that
+# move only weights carry the nontemporal cache policy (the 705 MB weight stream is read once;
+# the x rows gathered per in-edge stay cacheable)
+TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
@@ -299,14 +303,20 @@ def _glds_chunks(groups, nshp, node_off, wes: int = 4):
         need_l1 = sorted({p.l1 for p in grp})
         need_l2 = sorted({p.l2 for p in grp})
         chunks, fo_x, fo_w = [], {}, {}
+
+        def add_w():
+            for p in grp:
+                fo_w[p.slot] = 4 * len(chunks)
+                chunks.extend((2, wes * p.slot * MUL + 16 * cc) for cc in range(wes * MUL // 16))
+        if TP_FWD_WNT:
+            add_w()
         for l in need_l1:
             fo_x[l] = 4 * len(chunks)
             chunks += [(0, 4 * node_off[l] + 16 * cc) for cc in range(8 * (2 * l + 1))]
         fo_sh = 4 * len(chunks)
         chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
-        for p in grp:
-            fo_w[p.slot] = 4 * len(chunks)
-            chunks += [(2, wes * p.slot * MUL + 16 * cc) for cc in range(wes * MUL // 16)]
+        if not TP_FWD_WNT:
+            add_w()
         glist.append((need_l1, need_l2, chunks, fo_x, fo_sh, fo_w))
     return glist
 
@@ -418,9 +428,11 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
                 out.append(f"        const char* wb = ok_ ? reinterpret_cast<const char*>(w + (size_t)ee_ * {wn}) : pad_;")
                 out.append(f"        float4* dst = ib + ({buf}) * {2 * NI} + {h * NI};")
                 for j in range(nj):
+                    # cache policy 2 = nt on gfx950: an instruction that moves only weight chunks
+                    only_w = TP_FWD_WNT and all(k == 2 for k, _ in chunks[64 * j: 64 * j + 64])
                     out.append(f"        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)"
                                f"((kd{j} == 0 ? xb : kd{j} == 1 ? shb : wb) + of{j}), "
-                               f"(__attribute__((address_space(3))) void*)(dst + {64 * j}), 16, 0, 0);")
+                               f"(__attribute__((address_space(3))) void*)(dst + {64 * j}), 16, 0, {2 if only_w else 0});")
                 out.append("      }")
             out.append("    }")
             return out
