@@ -49,8 +49,9 @@ TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
 TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 # LDS-DMA tp_fwd: a group's weight slices lead its chunk list, and the LDS-DMA instructions that
 # move only weights carry the nontemporal cache policy (the 705 MB weight stream is read once;
-# the x rows gathered per in-edge stay cacheable)
-TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "0"))
+# the x rows gathered per in-edge stay cacheable).  r04t: in the step 0.418 -> 0.410 ms per launch
+# (roofline 0.535 -> 0.545), kbench 0.500 -> 0.492 ms; the step unchanged
+TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "1"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
