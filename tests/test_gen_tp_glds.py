@@ -4,8 +4,9 @@ The kernel moves one half-wave's rows for one edge as a static list of 16-byte c
 chunks per ``global_load_lds_dwordx4`` wave-instruction, and reads its operands back from the
 lane-linear image at the float offsets the generator recorded.  For every generated TP set this
 checks that the chunk list:
-* covers, exactly once and in order, the x blocks of the group's l1 values, the whole padded SH
-  row and the 32-float weight slice of every path of the group;
+* covers, exactly once and in order, the group's 32-float weight slices (first when
+  ``TP_FWD_WNT``: the weight-only LDS-DMA instructions then carry the nontemporal policy), the
+  x blocks of the group's l1 values and the whole padded SH row;
 * has every source piece 16-byte aligned and inside its row (x: din, SH: the padded nshp,
   w: wn floats), so no LDS-DMA load leaves the tensors it reads;
 * fits the image the kernel declares (ceil(chunks / 64) instructions of 64 chunks) and the
@@ -46,14 +47,20 @@ def test_chunk_lists_cover_the_rows_once_and_stay_in_bounds(name):
             gk._glds_chunks(groups, nshp, node_off), groups):
         assert need_l1 == sorted({p.l1 for p in grp})
         expect = []
+
+        def weights():
+            for p in grp:
+                assert fo_w[p.slot] == 4 * len(expect)
+                expect.extend((2, 4 * gk.MUL * p.slot + 16 * c) for c in range(8))
+        if gk.TP_FWD_WNT:
+            weights()
         for l in need_l1:
             assert fo_x[l] == 4 * len(expect)
             expect += [(0, 4 * node_off[l] + 16 * c) for c in range(8 * (2 * l + 1))]
         assert fo_sh == 4 * len(expect)
         expect += [(1, 16 * c) for c in range(nshp // 4)]
-        for p in grp:
-            assert fo_w[p.slot] == 4 * len(expect)
-            expect += [(2, 4 * gk.MUL * p.slot + 16 * c) for c in range(8)]
+        if not gk.TP_FWD_WNT:
+            weights()
         assert chunks == expect
         row_bytes = {0: 4 * din, 1: 4 * nshp, 2: 4 * wn}
         for kind, off in chunks:
