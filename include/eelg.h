@@ -300,7 +300,7 @@ int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_r
  * eelg_linear_bwd_w, eelg_radial_bwd and eelg_sc_bwd_coef, and the bias gradients = column
  * sums of grad_out; replaces the reference's implicit autograd reductions, gnn/blocks.py and
  * e3nn o3.Linear biases): out[c] = scale * sum_{r < rows} part[r*ld + c] for c < cols, rows
- * summed in a fixed order.  rows > 2048 needs a workspace of eelg_sum_rows_work(rows, cols)
+ * summed in a fixed order.  rows > 256 needs a workspace of eelg_sum_rows_work(rows, cols)
  * floats (0 otherwise).  16-byte aligned part / out with ld, cols multiples of 4 take the
  * float4 path.  -2 on bad sizes. */
 long long eelg_sum_rows_work(int rows, long long cols);
