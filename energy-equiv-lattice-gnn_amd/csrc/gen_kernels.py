@@ -52,6 +52,9 @@ TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 # the x rows gathered per in-edge stay cacheable).  r04t: in the step 0.418 -> 0.410 ms per launch
 # (roofline 0.535 -> 0.545), kbench 0.500 -> 0.492 ms; the step unchanged
 TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "1"))
+# LDS-DMA tp_fwd: the aggregate rows stored nontemporal (r03l/r03n with the register pipeline:
+# the kernel 3 % faster, the step 0.4 % slower as the following linear missed in L2)
+TP_FWD_ANT = int(os.environ.get("EELG_TP_FWD_ANT", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
@@ -508,7 +511,7 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
             for p in grp:
                 d3 = 2 * p.l3 + 1
                 L.extend("          " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                             f"{p.out_off} + u * {d3}"))
+                                                             f"{p.out_off} + u * {d3}", nt=bool(TP_FWD_ANT)))
             L.append("          " + " ".join(f"{a} = 0.0f;" for a in accs))
             L.append("        }")
             L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
