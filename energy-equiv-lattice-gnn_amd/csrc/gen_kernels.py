@@ -53,7 +53,8 @@ TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 # (roofline 0.535 -> 0.545), kbench 0.500 -> 0.492 ms; the step unchanged
 TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "1"))
 # LDS-DMA tp_fwd: the aggregate rows stored nontemporal (r03l/r03n with the register pipeline:
-# the kernel 3 % faster, the step 0.4 % slower as the following linear missed in L2)
+# the kernel 3 % faster, the step 0.4 % slower as the following linear missed in L2; r04w: kbench
+# 0.491 -> 0.469 ms, but in the step the kernel itself 0.406 -> 0.418 ms and the step equal)
 TP_FWD_ANT = int(os.environ.get("EELG_TP_FWD_ANT", "0"))
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
