@@ -41,10 +41,9 @@ TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 # in the step 0.438 vs 0.446 ms)
 TP_FWD_WPB = int(os.environ.get("EELG_TP_FWD_WPB", "1"))
 # tp_fwd: the rows of the next two edges (x / SH / weight) prefetched into LDS by LDS-DMA
-# (global_load_lds) instead of a second register set, for fp32 and bf16 weight storage; 0 = the
-# register pipeline.  One edge in flight by LDS-DMA measured slower
-# (r03ag/r03ai: 0.499 vs 0.486 ms kbench) and was removed.
-TP_FWD_GLDS = int(os.environ.get("EELG_TP_FWD_GLDS", "2"))
+# (global_load_lds) instead of a second register set, for fp32 and bf16 weight storage.  One
+# edge in flight by LDS-DMA (r03ag/r03ai: 0.499 vs 0.486 ms kbench) and the register pipeline
+# (0.513 ms; 0.439 vs 0.418 ms in the step) were removed.
 # LDS-DMA tp_fwd: minimum waves per SIMD asked of the register allocator (0: none)
 TP_FWD_WPE = int(os.environ.get("EELG_TP_FWD_WPE", "0"))
 # LDS-DMA tp_fwd: a group's weight slices lead its chunk list, and the LDS-DMA instructions that
@@ -565,117 +564,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # the ngroups path-group blocks of one node tile share blockIdx.x % 8, i.e. one XCD,
     # and read the tile's x rows / SH rows / indices through one L2.
     ng = len(groups)
-    if TP_FWD_GLDS == 2:
-        L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf)
-    else:
-        L.append(f"__global__ __launch_bounds__({64 * TP_FWD_WPB}) void tp_fwd_{name}{sfx}(")
-        L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
-        L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
-        L.append("    float inv_norm, float* __restrict__ agg) {")
-        L.append("  const int lane = threadIdx.x & 63;")
-        L.append(f"  const int u = lane & {MUL - 1};")
-        # XCD k (blockIdx % 8) takes one contiguous range of node tiles, walked in order: the x
-        # rows of a lattice are gathered by one XCD (its L2) rather than by all eight (r03h: 1828
-        # -> 1865 graphs/s together with the 64-accumulator groups)
-        TN = 2 * TP_FWD_WPB * TP_NPH          # receivers per node tile (one workgroup)
-        L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
-        L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
-        L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
-        L.append(f"  const int n0 = ((tile * {TP_FWD_WPB} + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {TP_NPH};")
-        L.append("  if (n0 >= n_nodes) return;")
-        L.append(f"  const int n1 = min(n0 + {TP_NPH}, n_nodes);")
-        L.append("  switch (grp) {")
-        for gi, grp in enumerate(groups):
-            L.append(f"  case {gi}: {{")
-            need_l1 = sorted({p.l1 for p in grp})
-            need_l2 = sorted({p.l2 for p in grp})
-            accs = [f"a{p.slot}_{k}" for p in grp for k in range(2 * p.l3 + 1)]
-            L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
-            cur = ([f"x{l}_{i}" for l in need_l1 for i in range(2 * l + 1)]
-                   + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
-                   + [f"w{p.slot}" for p in grp])
-
-            def load(pref, ev, sv, guard):
-                # a missing edge reads the pad row (x row 0 exists since N > 0, but no edge row
-                # need exist: E = 0); the loaded values of a missing edge are never used
-                out = [f"    {{ const bool ok = {guard};",
-                       f"      const float* __restrict__ xs = x + (size_t){sv} * {din};",
-                       f"      const float* __restrict__ ye = ok ? sh + (size_t){ev} * {nshp} : eelg_tp_pad;",
-                       f"      const {WT}* __restrict__ we = (ok ? w + (size_t){ev} * {wn} : "
-                       f"reinterpret_cast<const {WT}*>(eelg_tp_pad)) + u;"]
-                for l in need_l1:
-                    d = 2 * l + 1
-                    out += ["      " + ln for ln in vec_load([f"{pref}x{l}_{i}" for i in range(d)], "xs",
-                                                              f"{node_off[l]} + u * {d}")]
-                out += ["      " + ln for ln in sh_load(need_l2, pref, "ye")]
-                for p in grp:
-                    out.append(f"      {pref}w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
-                out.append("    }")
-                return out
-            L.append("    int e = rowptr[n0];")
-            L.append("    const int eend = rowptr[n1];")
-            L.append("    int node = n0, nend = rowptr[n0 + 1], nend2 = rowptr[min(n0 + 2, n1)];")
-            L.append("    int s1 = e + 1 < eend ? sender[e + 1] : 0;")
-            L.append("    float " + ", ".join(cur) + ";")
-            L += load("", "e", "(e < eend ? sender[e] : 0)", "e < eend")
-            gpin = pin(accs + cur)
-            def step(cp, np_):
-                """one pipelined edge step: flush finished receivers, issue edge e+1's loads
-                into the ``np_`` register set, compute edge e from the ``cp`` set"""
-                out = []
-                # flush every receiver whose range ends here (also covers receivers with no in-edges)
-                out.append("      while (node < n1 && nend == e) {")
-                out.append(f"        float* __restrict__ o = agg + (size_t)node * {dmid};")
-                for p in grp:
-                    d3 = 2 * p.l3 + 1
-                    out.extend("        " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                                 f"{p.out_off} + u * {d3}"))
-                out.append("        " + " ".join(f"{a} = 0.0f;" for a in accs))
-                out.append("        ++node; nend = nend2; nend2 = rowptr[min(node + 2, n1)];")
-                out.append("      }")
-                out.append("      if (e >= eend) break;")
-                out.append("      { const int s2 = e + 2 < eend ? sender[e + 2] : 0;")
-                out.extend("  " + ln for ln in load(np_, "e + 1", "s1", "e + 1 < eend"))
-                cpin = pin(accs + [cp + v for v in cur] + [np_ + v for v in cur])
-                # the in-flight next-edge registers are pinned only after the last path, so no
-                # earlier path boundary waits for the prefetch to land
-                cpin_mid = pin(accs + [cp + v for v in cur])
-                xn = lambda p, i: f"{cp}x{p.l1}_{i}"  # noqa: E731
-                yn = lambda p, j: f"{cp}y{p.l2 * p.l2 + j}"  # noqa: E731
-                for p in grp:
-                    d1, d2, d3 = 2 * p.l1 + 1, 2 * p.l2 + 1, 2 * p.l3 + 1
-                    out.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
-                    out.append(f"        const float wp = {cp}w{p.slot} * ({flit(p.coef)} * inv_norm);")
-                    fold = min((d3 + 1, "none"), (d1, "x"), (d2, "y"))
-                    if fold[1] == "none":
-                        _emit_t(p, xn, yn, "t", out, "        ")
-                        for k in range(d3):
-                            out.append(f"        a{p.slot}_{k} = fmaf(wp, t{k}, a{p.slot}_{k});")
-                    else:
-                        # fold the path weight into the shorter of x / y (d1 or d2 products instead
-                        # of d3 + 1) and accumulate the CG terms straight into the accumulators
-                        if fold[1] == "x":
-                            for i in range(d1):
-                                out.append(f"        const float xw{i} = {xn(p, i)} * wp;")
-                            xf, yf = (lambda p, i: f"xw{i}"), yn
-                        else:
-                            for j in range(d2):
-                                out.append(f"        const float yw{j} = {yn(p, j)} * wp;")
-                            xf, yf = xn, (lambda p, j: f"yw{j}")
-                        _emit_acc(p, xf, yf, lambda k, p=p: f"a{p.slot}_{k}", out, "        ")
-                    out.append("      }")
-                    out.append("      " + (cpin if p is grp[-1] else cpin_mid))
-                out.append("      s1 = s2; ++e; }")
-                return out
-            L.append("    for (;;) {")
-            L.append("      float " + ", ".join("n" + v for v in cur) + ";")
-            L += step("", "n")
-            L.append("      " + " ".join(f"{v} = n{v};" for v in cur))
-            L.append("    }")
-            L.append("    break; }")
-        L.append("  default: break;")
-        L.append("  }")
-        L.append("}")
+    L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf)
 
     # ---------------- backward (per edge) ----------------
     # grouped by input block l1: each group owns a disjoint slice of gxe, so no
