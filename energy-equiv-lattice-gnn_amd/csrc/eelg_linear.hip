@@ -270,10 +270,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LIN_FWD_WPE
 // (node, m) rows: row r = (n, m) sits at n*32*D + m, and lane u reads x[r][u] at + u*D, an odd
 // stride (D = 2l+1) over the 32 banks, so the operand reads are conflict-free too.  Rows past
 // NB*D point at a zeroed node region.  Same partial layout as the general path.
-// LINW_PFD: node chunks in flight per wave in the fast grad-W (1: one register set; 2: two)
-#ifndef LINW_PFD
-#define LINW_PFD 1
-#endif
 template <int D>
 __device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x_row,
                                               const float* __restrict__ g, int g_row, int n0,
@@ -310,44 +306,6 @@ __device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x
     }
   };
   int nc = n0 + wave * NB;
-#if LINW_PFD == 2
-  // two chunks in flight: register sets (rx, rg) and (sx, sg) alternate, chunk c + 2 is issued
-  // into the set chunk c was just staged from
-  float4 sx[NQ], sg[NQ];
-  auto load_into = [&](int ncc, float4* ax, float4* ag) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int f = lane + 64 * q;
-      const int a = f / RUN4, w4 = f - a * RUN4;
-      const bool ok = f < NB * RUN4 && ncc + a < n1;
-      const int nn = ok ? ncc + a : 0;
-      ax[q] = ok ? *reinterpret_cast<const float4*>(xb + (size_t)nn * x_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      ag[q] = ok ? *reinterpret_cast<const float4*>(gb + (size_t)nn * g_row + 4 * w4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto consume = [&](int ncc, float4* ax, float4* ag) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int f = lane + 64 * q;
-      if (f < NB * RUN4) {
-        reinterpret_cast<float4*>(xw)[f] = ax[q];
-        reinterpret_cast<float4*>(gw)[f] = ag[q];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (ncc + 8 * NB < n1) load_into(ncc + 8 * NB, ax, ag);
-#pragma unroll
-    for (int st = 0; st < 16; ++st)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[off[st]], gw[off[st]], acc, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();
-  };
-  if (nc < n1) load_into(nc, rx, rg);
-  if (nc + 4 * NB < n1) load_into(nc + 4 * NB, sx, sg);
-  for (; nc < n1; nc += 8 * NB) {
-    consume(nc, rx, rg);
-    if (nc + 4 * NB < n1) consume(nc + 4 * NB, sx, sg);
-  }
-#else
   if (nc < n1) load_chunk(nc);
   for (; nc < n1; nc += 4 * NB) {
 #pragma unroll
@@ -365,7 +323,6 @@ __device__ __forceinline__ void lin_bwdw_fast(const float* __restrict__ x, int x
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xw[off[st]], gw[off[st]], acc, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
   }
-#endif
 }
 
 #ifndef LIN_BWDW_WPE
