@@ -375,6 +375,9 @@ def main():
     ap.add_argument("--check-params", action="store_true",
                     help="N > 1: check after the timed steps that every rank holds bitwise-equal "
                          "parameters (reported as params_equal_across_ranks)")
+    ap.add_argument("--node-order", default="none", choices=["none", "morton", "auto"],
+                    help="collate-time node numbering within each graph: as generated, Morton "
+                         "(Z-order of the positions), or auto = Morton for graphs over 2048 nodes")
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="2 = BASELINE configs[1] (default); 5 = configs[4]: lmax 3, ~5k-node "
                          "lattices (5000 nodes / 20000 edges), bf16 storage, fp32 accumulate")
@@ -399,6 +402,12 @@ def main():
     # graphs rank*B .. rank*B+B-1 (graph-sharded, seed 1234 + global graph id)
     ds = SyntheticLattices(args.batch * world, args.nodes, args.edges, 1234)
     mine = [ds[rank * args.batch + g] for g in range(args.batch)]
+    if args.node_order == "morton" or (args.node_order == "auto" and args.nodes > 2048):
+        from gnn.data import morton_order, reorder_nodes
+        mine = [reorder_nodes(d, morton_order(d.positions)) for d in mine]
+        args.node_order = "morton"
+    else:
+        args.node_order = "as generated"
     rmax = torch.tensor([max(float(d.edge_attr.max()) for d in mine)], device=dev)
     if world > 1:
         dist.all_reduce(rmax, op=dist.ReduceOp.MAX)
@@ -492,6 +501,7 @@ def main():
                                    "fwd+loss+bwd+allreduce+clip+AdamW",
                        "global_batch": args.batch * world, "nodes_per_graph": args.nodes,
                        "edges_per_graph": args.edges, "layers": args.layers,
+                       "node_order": args.node_order,
                        "parallelism": f"graph-sharded dp{world}"},
             "backend": backend, "rehearsal": backend == "gloo",
             "loss": round(float(loss.item()), 6),

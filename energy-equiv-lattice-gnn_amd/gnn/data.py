@@ -93,6 +93,37 @@ def collate(data_list: List[Data]) -> Batch:
     return Batch.from_data_list(data_list)
 
 
+def morton_order(positions: torch.Tensor, bits: int = 10) -> torch.Tensor:
+    """Node permutation along a Morton (Z-order) curve of the positions (quantised to
+    ``bits`` per axis over the graph's bounding box): spatial neighbours get nearby ids."""
+    pos = positions.detach().double().cpu()
+    lo, hi = pos.min(0).values, pos.max(0).values
+    scale = (1 << bits) - 1
+    q = ((pos - lo) / (hi - lo).clamp_min(1e-12) * scale).long().clamp(0, scale)
+    key = torch.zeros(pos.shape[0], dtype=torch.long)
+    for bit in range(bits):
+        for ax in range(3):
+            key |= ((q[:, ax] >> bit) & 1) << (3 * bit + ax)
+    return torch.argsort(key, stable=True)
+
+
+def reorder_nodes(d: Data, perm: torch.Tensor) -> Data:
+    """The same graph with node ``perm[i]`` renumbered ``i``: node tensors gathered, edge
+    endpoints remapped, edges (and their shifts / radii) kept in order.  Graph-level outputs of
+    the model are invariant (message passing is permutation-equivariant); the interaction
+    kernels gather ``x[sender]`` from a smaller window of rows when neighbours have nearby ids
+    (DESIGN.md section 6, config 5)."""
+    import copy
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel())
+    e = copy.copy(d)
+    for k in _NODE_KEYS:
+        if k in d:
+            e[k] = d[k][perm]
+    e.edge_index = inv[d.edge_index]
+    return e
+
+
 def build_edge_csr(edge_index: torch.Tensor, num_nodes: int) -> Dict[str, torch.Tensor]:
     """Receiver-sorted edge order + CSR, and sender-CSR over that order.
 
