@@ -507,6 +507,7 @@ def main():
             "loss": round(float(loss.item()), 6),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
         }
         if same is not None:
             out["params_equal_across_ranks"] = same
