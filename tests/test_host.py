@@ -316,3 +316,20 @@ def test_packed_linear_rule_keeps_short_k_on_fp32_kernels():
     assert big._pk_ok == {"fwd": True, "bx": False}
     sq = o3.Linear("32x0e+32x1o+32x2e+32x3o+32x4e", "32x0e+32x1o+32x2e+32x3o+32x4e")
     assert sq._pk_ok == {"fwd": False, "bx": False}
+
+
+def test_morton_reorder_keeps_every_edge_vector():
+    """``reorder_nodes(d, morton_order(d.positions))`` is a relabelling: node tensors are
+    permuted, each edge keeps its endpoints' positions (so its vector and strut) and its order,
+    and neighbours get nearby ids."""
+    from gnn.data import morton_order, reorder_nodes
+    d = make_lattice(600, 2400, 5)
+    perm = morton_order(d.positions)
+    assert torch.equal(torch.sort(perm).values, torch.arange(600))
+    e = reorder_nodes(d, perm)
+    assert torch.equal(e.positions, d.positions[perm]) and torch.equal(e.node_attrs, d.node_attrs[perm])
+    v0 = d.positions[d.edge_index[1]] - d.positions[d.edge_index[0]]
+    v1 = e.positions[e.edge_index[1]] - e.positions[e.edge_index[0]]
+    assert torch.equal(v0, v1) and torch.equal(e.shifts, d.shifts) and torch.equal(e.edge_attr, d.edge_attr)
+    gap = lambda g: (g.edge_index[0] - g.edge_index[1]).abs().double().mean()  # noqa: E731
+    assert gap(e) < 0.5 * gap(d)
