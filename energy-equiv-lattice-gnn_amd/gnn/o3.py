@@ -22,8 +22,11 @@ from . import cg
 from .irreps import Irreps
 
 # grad-W launch shape: target workgroups and a cap on the node slices (partials)
-LINW_WG = int(os.environ.get("EELG_LINW_WG", "1024"))
-LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "64"))
+# r04ac kbench: 1024 / 64 -> 4096 / 128 takes grad-W 7360 -> 800 from 0.324 to 0.264 ms and
+# 800 -> 800 from 0.056 to 0.049 ms (a grid of about one round left the D = 9 tiles, 9x the
+# bytes per node of D = 1, as the tail); the step is unchanged (these run on a side stream)
+LINW_WG = int(os.environ.get("EELG_LINW_WG", "4096"))
+LINW_MAX_SLICES = int(os.environ.get("EELG_LINW_MAX_SLICES", "128"))
 # forward / grad-x of the eligible linears on bf16 MFMA with fp32-accurate split operands (1),
 # or on the fp32 MFMA kernels (0).  Only descriptors whose every slot sums K >= LIN_X6_MINK take
 # it: r04b kbench, 7360->800 fwd (K 160..320) 0.261 vs 0.290 ms fp32; K = 32 (the 800->800
