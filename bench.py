@@ -135,7 +135,11 @@ def pmc_traffic(kernel: str, args) -> dict | None:
     tab = json.load(open(path)).get("workloads", {}).get(workload_key(args))
     if tab is None:
         return None
-    hits = [v for k, v in tab["kernels"].items() if k.split("|")[0] == kernel]
+    def base(name):   # "void cgc_fwd_kernel<2>" -> "cgc_fwd_kernel"
+        name = name.split("|")[0]
+        name = name[5:] if name.startswith("void ") else name
+        return name.split("<")[0]
+    hits = [v for k, v in tab["kernels"].items() if base(k) == kernel]
     if not hits:
         return None
     t = max(hits, key=lambda v: sum(v.values()))
@@ -469,10 +473,12 @@ def main():
                                 2 if args.storage == "bfloat16" else 4)
             ms = ksum[key]["mean_ms"]
             ach = byts / (ms * 1e-3) / 1e9
+            # the generated kernel's name (the bf16-storage form carries the _bw suffix)
+            kname = f"tp_fwd_tpB_l{args.lmax}" + ("_bw" if args.storage == "bfloat16" else "")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4),
-                    "traffic": None, "traffic_detail": pmc_traffic(f"tp_fwd_tpB_l{args.lmax}", args),
-                    "kernel": f"tp_fwd_tpB_l{args.lmax} (fused gather+TP+segmented sum)",
+                    "traffic": None, "traffic_detail": pmc_traffic(kname, args),
+                    "kernel": f"{kname} (fused gather+TP+segmented sum)",
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum[key]["count"]}
             if roof["traffic_detail"]:
                 roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)

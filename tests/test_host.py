@@ -333,3 +333,25 @@ def test_morton_reorder_keeps_every_edge_vector():
     assert torch.equal(v0, v1) and torch.equal(e.shifts, d.shifts) and torch.equal(e.edge_attr, d.edge_attr)
     gap = lambda g: (g.edge_index[0] - g.edge_index[1]).abs().double().mean()  # noqa: E731
     assert gap(e) < 0.5 * gap(d)
+
+
+def test_bench_traffic_lookup_finds_every_workloads_roofline_kernel():
+    """bench.py's roofline ``traffic`` comes from the committed PMC table under the command's
+    workload key; the kernel names it looks up must match the traced names (the bf16-storage
+    forward carries ``_bw``, the CGC forward is a template)."""
+    import importlib.util
+    import os
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("_bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    A = types.SimpleNamespace
+    cases = [(A(model="egnn", batch=32, nodes=1024, edges=4096, layers=4, lmax=4, storage="float32"),
+              "tp_fwd_tpB_l4"),
+             (A(model="egnn", batch=32, nodes=5000, edges=20000, layers=4, lmax=3, storage="bfloat16"),
+              "tp_fwd_tpB_l3_bw"),
+             (A(model="cgc_modified", batch=256, nodes=1024, edges=4096), "cgc_fwd_kernel")]
+    for args, kernel in cases:
+        t = bench.pmc_traffic(kernel, args)
+        assert t is not None and t["bytes"] > 1e9, (bench.workload_key(args), kernel)
