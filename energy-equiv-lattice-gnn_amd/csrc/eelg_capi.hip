@@ -595,8 +595,11 @@ int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* s
                  void* stream) {
   if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
   if (n_nodes <= 0) return 0;
-  if (D > 128) return fail(-2, "cgc_fwd: D = %d > 128 not built", D);
-  if (D > 64)
+  if (D > EELG_CGC_MAXD) return fail(-2, "cgc_fwd: D = %d > %d not built", D, EELG_CGC_MAXD);
+  if (D > 128)
+    hipLaunchKernelGGL(cgc_fwd_kernel<4>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
+  else if (D > 64)
     hipLaunchKernelGGL(cgc_fwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
                        pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
   else
@@ -610,8 +613,11 @@ int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* s
                  const float* grad_agg, float* dz, float* grad_pr, void* stream) {
   if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
   if (n_nodes <= 0) return 0;
-  if (D > 128) return fail(-2, "cgc_bwd: D = %d > 128 not built", D);
-  if (D > 64)
+  if (D > EELG_CGC_MAXD) return fail(-2, "cgc_bwd: D = %d > %d not built", D, EELG_CGC_MAXD);
+  if (D > 128)
+    hipLaunchKernelGGL(cgc_bwd_kernel<4>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
+                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
+  else if (D > 64)
     hipLaunchKernelGGL(cgc_bwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
                        pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
   else

@@ -94,6 +94,7 @@ class LinWDesc(ctypes.Structure):
 
 RADIAL_MAXH = 3
 GATE_MAXBLK = 8
+CGC_MAXD = 256           # include/eelg.h EELG_CGC_MAXD
 GATE_MAXGATED = 2048     # include/eelg.h EELG_GATE_MAXGATED / EELG_GATE_MAXGATES
 GATE_MAXGATES = 512
 

@@ -84,6 +84,9 @@ class CGCLayer(torch.nn.Module):
         if edge_dim != node_dim:
             raise NotImplementedError("CGCLayer: the fused kernel needs edge_dim == node_dim "
                                       "(as in both reference models)")
+        if node_dim > _lib.CGC_MAXD:
+            raise NotImplementedError(f"CGCLayer: node_dim {node_dim} > {_lib.CGC_MAXD}, the widest "
+                                      "built CGC kernel (include/eelg.h EELG_CGC_MAXD)")
         if reduction not in ("sum", "mean"):
             raise NotImplementedError(f"CGCLayer reduction {reduction!r}")
         self.num_hid_dim = 2 * node_dim + edge_dim

@@ -186,6 +186,12 @@ class Linear(torch.nn.Module):
             _accept_empty(state_dict, prefix + "bias", error_msgs)
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                       unexpected_keys, error_msgs)
+        self.invalidate_packed()
+
+    def invalidate_packed(self) -> None:
+        """forget the packed split weights (after a write the version counter does not see)"""
+        if hasattr(self, "_pk_cache"):
+            self._pk_cache.clear()
 
     # -- descriptor tables for the C ABI (built once) ---------------------------
     def _build_descriptors(self):
@@ -269,7 +275,9 @@ class Linear(torch.nn.Module):
 
     def _packed(self, which: str, weight):
         """split, alpha-scaled weights of descriptor ``which`` ('fwd' or 'bx') for the packed
-        kernel, rebuilt when the weight changes (cached per weight version)"""
+        kernel, rebuilt when the weight changes (cached per weight version).  A write through
+        ``weight.data`` does not bump the version counter: such writers call
+        ``invalidate_packed()`` (``parallel.broadcast_parameters`` and ``load_state_dict`` do)."""
         from . import _lib
         key = (weight.data_ptr(), weight._version, weight.device)
         hit = self._pk_cache.get(which)
@@ -286,7 +294,8 @@ class Linear(torch.nn.Module):
     def _run_pk(self, which, x, x_row, weight, bias, extra, n, out, out_row, desc) -> bool:
         """the packed launch when eligible; False leaves the call to the fp32 kernels"""
         from . import _lib
-        if not (LIN_X6 and self._pk_ok[which] and x.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
+        if not (LIN_X6 and self._pk_ok[which] and x_row % 4 == 0 and out_row % 4 == 0
+                and x.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
                 and (extra is None or extra.data_ptr() % 16 == 0)):
             return False
         pk = self._packed(which, weight.detach())

@@ -75,3 +75,9 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> N
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=src, group=group)
+    # writes through .data leave the version counters alone: drop the weight-derived caches
+    # (the split-bf16 packed weights of o3.Linear) so the next forward re-derives them
+    for m in module.modules():
+        inv = getattr(m, "invalidate_packed", None)
+        if inv is not None:
+            inv()

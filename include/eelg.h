@@ -171,6 +171,7 @@ int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, 
  * then multipliers), ep = edge_ft W_e^T ([E, 2D], receiver-sorted edge order).
  * agg[n] = row_scale[n] * sum_e softplus(zv) sigmoid(zm)  (row_scale NULL -> 'sum').
  * Built for D <= 128 (the benchmark models use 128 and 64); -2 otherwise. */
+#define EELG_CGC_MAXD 256   /* node_dim of the built CGC kernels (one lane per 64 channels, <= 4) */
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
                  void* stream);

@@ -517,7 +517,7 @@ def test_gate_fused_matches_oracle(scal, gates, gated):
     assert ey < 1e-6 and ex < 1e-6, (ey, ex)
 
 
-@pytest.mark.parametrize("reduce", ["sum", "add", "max", "min", "mul"])
+@pytest.mark.parametrize("reduce", ["sum", "add", "max", "min"])
 def test_model_global_reductions_match_oracle(reduce):
     """``global_reduction`` is any torch_scatter reduce (gnn/model.py:100-106); same
     tolerances as the mean case above (1e-4 stiffness / loss, 1e-5 gradients)."""
@@ -539,6 +539,53 @@ def test_model_global_reductions_match_oracle(reduce):
     po = dict(o.named_parameters())
     worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
     record_parity(f"model_reduce_{reduce}", stiffness=rel_err(cm, co), grad_params=worst)
+    assert rel_err(cm, co) < 1e-4
+    assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
+    assert worst < 1e-5
+
+
+def test_model_global_reduction_mul_is_not_degenerate():
+    """``global_reduction='mul'`` (gnn/model.py:100-106): a product over a 50-node graph's
+    readout features (|x| ~ 1e-2) underflows to ~0, so the stiffness is then a constant and the
+    comparison checks nothing.  Here the graphs have 4 nodes and the readout's last linear is
+    scaled 30x, so the pooled products are O(1e-3 .. 1e4) (asserted) and every node's features
+    reach the output; stiffness / loss 1e-4, every parameter gradient 1e-5 of its max."""
+    import oracle.model as om
+    from gnn.model import EnergyEquivGNN
+    from gnn.train import stiffness_loss
+    b, rmax = batch(4, 4, 8, 11)
+    bd = b.to(DEV)
+    p = params(2, max_edge_radius=rmax, global_reduction="mul")
+    torch.manual_seed(0)
+    o = omodel.EnergyEquivGNN(p).double()
+    with torch.no_grad():
+        o.stiffness_head.nonlin_readout.linear_2.weight.mul_(30.0)
+    m = EnergyEquivGNN(p).to(DEV)
+    copy_params(o, m)
+    cap = {}
+    pool = om.scatter_reduce_order
+
+    def spy(src, index, n, red):
+        out = pool(src, index, n, red)
+        cap["pooled"] = out.detach()
+        return out
+    bo = batch_to(b, "cpu", torch.float64)
+    om.scatter_reduce_order = spy
+    try:
+        co = o(bo)["stiffness"]
+    finally:
+        om.scatter_reduce_order = pool
+    lo = oracle_loss(co, bo.stiffness)
+    lo.backward()
+    cm = m(bd)["stiffness"]
+    lm = stiffness_loss(cm, bd.stiffness)
+    lm.backward()
+    g = cap["pooled"].abs()
+    po = dict(o.named_parameters())
+    worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
+    record_parity("model_reduce_mul", stiffness=rel_err(cm, co), grad_params=worst,
+                  pooled_median=float(g.median()), pooled_max=float(g.max()))
+    assert float(g.median()) > 1e-4 and float(g.max()) > 1.0, (float(g.median()), float(g.max()))
     assert rel_err(cm, co) < 1e-4
     assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
     assert worst < 1e-5

@@ -28,6 +28,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEFAULT_WK = "egnn_b32_n1024_e4096_L4_lmax4_float32"
 
 
+def _last_json(path):
+    """the last JSON line of a file (the bench line), or None"""
+    if not os.path.exists(path):
+        return None
+    for line in reversed(open(path).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+def _timed_region_launches(path, kernel, n):
+    """durations (ns) of the last ``n`` launches of ``kernel`` in a rocprofv3 kernel trace: the
+    launches of bench.py's timed region (its warm-up launches come first)"""
+    if not n or not os.path.exists(path):
+        return None
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(path))
+         if r["Kernel_Name"].split("(")[0] == kernel]
+    return d[-n:] if len(d) >= n else None
+
+
+def _stats_avg(rows, kernel):
+    hit = [r for r in rows if r["Name"].split("(")[0] == kernel]
+    return float(hit[0]["AverageNs"]) if hit else float("nan")
+
+
 def main(src, tag, wk=DEFAULT_WK):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -37,15 +62,34 @@ def main(src, tag, wk=DEFAULT_WK):
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     bench = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
     b = json.loads(bench)
-    steps_traced = 7           # profile_round.sh: --steps 5 --warmup 2
+    tb = _last_json(os.path.join(src, "trace.json"))
+    steps_traced = (tb["steps"] + tb["warmup"]) if tb else 7
+    rk = b["roofline"]["kernel"].split()[0]
+    timed = _timed_region_launches(os.path.join(src, "trace", "run_kernel_trace.csv"), rk,
+                                   tb["roofline"]["launches"] if tb else None)
+    byts = b["roofline"]["bytes_per_launch"]
     lines = [f"# Profile {tag}", "",
-             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 "
-             "--no-cpu-baseline` (7 traced steps); bench line from `python3 bench.py --steps "
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps "
+             f"{tb['steps'] if tb else 5} --warmup {tb['warmup'] if tb else 2} --no-cpu-baseline` "
+             f"({steps_traced} traced steps); bench line from `python3 bench.py --steps "
              f"{b['steps']} --warmup {b['warmup']}` on the same box.", "",
              f"bench: **{b['value']} {b['unit']}**, {b['ms_per_step']} ms/step; roofline kernel "
              f"{b['roofline']['kernel']}: {b['roofline']['mean_ms']} ms/launch (HIP events), "
-             f"{b['roofline']['achieved']} GB/s = {b['roofline']['frac']*100:.1f}% of 8 TB/s", "",
-             f"kernel time traced: {tot/1e6:.1f} ms = {tot/1e6/steps_traced:.2f} ms/step", "",
+             f"{b['roofline']['achieved']} GB/s = {b['roofline']['frac']*100:.1f}% of 8 TB/s", ""]
+    if tb and timed:
+        tr_ms = sum(timed) / len(timed) / 1e6
+        ev_ms = tb["roofline"]["mean_ms"]
+        lines += ["## Roofline kernel: HIP events vs the kernel trace", "",
+                  f"| measure | {rk} ms/launch | frac of 8 TB/s ({byts:,} B/launch) |", "|---|---|---|",
+                  f"| traced run, trace timestamps, the {len(timed)} timed-region launches | "
+                  f"{tr_ms:.4f} | {byts / (tr_ms * 1e-3) / 8e12:.4f} |",
+                  f"| traced run, HIP events of the same launches (bench line of the traced process: "
+                  f"{tb['value']} {tb['unit']}) | {ev_ms:.4f} | {tb['roofline']['frac']:.4f} |",
+                  f"| untraced run, HIP events (bench line above) | {b['roofline']['mean_ms']:.4f} | "
+                  f"{b['roofline']['frac']:.4f} |",
+                  f"| traced run, rocprofv3 --stats average (all launches incl. warm-up) | "
+                  f"{_stats_avg(rows, rk) / 1e6:.4f} | {byts / (_stats_avg(rows, rk) * 1e-9) / 8e12:.4f} |", ""]
+    lines += [f"kernel time traced: {tot/1e6:.1f} ms = {tot/1e6/steps_traced:.2f} ms/step", "",
              "| % | calls/step | avg us | kernel |", "|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
         lines.append(f"| {float(r['TotalDurationNs'])/tot*100:.1f} | {int(r['Calls'])/steps_traced:.1f} | "
