@@ -230,9 +230,10 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax:
 
 
 def cgc_fwd_bytes(n: int, e: int, d: int) -> int:
-    """Algorithmic bytes of one fused CGC edge-conv launch: node projections ps, pr [N, 2D]
-    and edge projections ep [E, 2D] read once, sender [E] + rowptr [N+1], agg [N, D] written."""
-    return 4 * (2 * n * 2 * d + e * 2 * d + e + (n + 1) + n * d)
+    """Algorithmic bytes of one fused CGC edge-conv launch on factored edge features
+    (``eelg_cgc_fwd_ef``, the models' path): node projections ps, pr [N, 2D] read once, the
+    8-float edge rows ef [E, 8] and A [8, 2D], sender [E] + rowptr [N+1], agg [N, D] written."""
+    return 4 * (2 * n * 2 * d + e * 8 + 8 * 2 * d + e + (n + 1) + n * d)
 
 
 def cpu_baseline_cgc(modified: bool, p, n_nodes: int, n_edges: int, budget_s: float):
@@ -327,7 +328,7 @@ def main_cgc(args):
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                     "traffic_detail": pmc_traffic("cgc_fwd_kernel", args),
-                    "kernel": "cgc_fwd (fused gather + softplus*sigmoid + segmented sum)",
+                    "kernel": "cgc_fwd (fused gather + factored edge projection + softplus*sigmoid + segmented sum)",
                     "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum["cgc_fwd"]["count"]}
             if roof["traffic_detail"]:
                 roof["traffic"] = roof["traffic_detail"]["bytes"]

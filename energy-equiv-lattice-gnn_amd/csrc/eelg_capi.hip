@@ -92,7 +92,12 @@ __device__ __forceinline__ float4 seg_load4(const unsigned short* __restrict__ r
 __device__ __forceinline__ float seg_load1(const float* __restrict__ p) { return *p; }
 __device__ __forceinline__ float seg_load1(const unsigned short* __restrict__ p) { return eelg_bf2f(*p); }
 
-template <bool VEC4, typename T>
+#ifndef SEG_EB
+#define SEG_EB 4     // source rows per batch of loads
+#endif
+// SEG_KMAX (template): float4 columns per lane, 1..4 (rows up to 1024 floats take the batched
+// path); 0 = the column loop
+template <bool VEC4, typename T, int SEG_KMAX = 0>
 __global__ __launch_bounds__(256) void segment_sum_kernel(
     const T* __restrict__ src, const int* __restrict__ rowptr, const int* __restrict__ idx,
     const float* __restrict__ row_scale, float scale, int n_rows, int width,
@@ -103,7 +108,49 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(
   const int beg = rowptr[row], end = rowptr[row + 1];
   const float sc = scale * (row_scale ? row_scale[row] : 1.0f);
   float* __restrict__ o = out + (size_t)row * width;
-  if (VEC4) {
+  if (VEC4 && SEG_KMAX > 0) {
+    // rows up to 64 * SEG_KMAX float4: a lane's SEG_KMAX columns of SEG_EB source rows are
+    // loaded at once (row indices first, then every column load), so up to SEG_EB * SEG_KMAX
+    // loads per lane are in flight instead of one dependent round trip per (column, row);
+    // the sums keep the row order, so results are bitwise those of the loop below
+    const int w4 = width >> 2;
+    constexpr int KM = SEG_KMAX > 0 ? SEG_KMAX : 1;
+    float4 acc[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j0 = beg; j0 < end; j0 += SEG_EB) {
+      int sr[SEG_EB];
+#pragma unroll
+      for (int q = 0; q < SEG_EB; ++q) {
+        const int j = min(j0 + q, end - 1);
+        sr[q] = idx ? idx[j] : j;
+      }
+      float4 v[SEG_EB][KM];
+#pragma unroll
+      for (int q = 0; q < SEG_EB; ++q)
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          const int c = min(lane + 64 * k, w4 - 1);
+          v[q][k] = seg_load4(src + (size_t)sr[q] * width, c);
+        }
+#pragma unroll
+      for (int q = 0; q < SEG_EB; ++q)
+        if (j0 + q < end)
+#pragma unroll
+          for (int k = 0; k < KM; ++k) {
+            acc[k].x += v[q][k].x; acc[k].y += v[q][k].y; acc[k].z += v[q][k].z; acc[k].w += v[q][k].w;
+          }
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int c = lane + 64 * k;
+      if (c < w4) {
+        float4 a = acc[k];
+        a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+        reinterpret_cast<float4*>(o)[c] = a;
+      }
+    }
+  } else if (VEC4) {
     const int w4 = width >> 2;
     for (int c = lane; c < w4; c += 64) {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -361,7 +408,16 @@ static int segment_sum_launch(const T* src, const int* rowptr, const int* idx,
   dim3 grid((n_rows + 3) / 4);
   const bool vec = (width % 4 == 0) && ((uintptr_t)src % (4 * sizeof(T)) == 0) &&
                    ((uintptr_t)out % 16 == 0);
-  if (vec)
+  const int km = vec ? (width / 4 + 63) / 64 : 0;
+#define SEG_LAUNCH(K) hipLaunchKernelGGL((segment_sum_kernel<true, T, K>), grid, dim3(256), 0, \
+                                         (hipStream_t)stream, src, rowptr, idx, row_scale, scale, \
+                                         n_rows, width, out)
+  if (vec && km == 1) SEG_LAUNCH(1);
+  else if (vec && km == 2) SEG_LAUNCH(2);
+  else if (vec && km == 3) SEG_LAUNCH(3);
+  else if (vec && km == 4) SEG_LAUNCH(4);
+#undef SEG_LAUNCH
+  else if (vec)
     hipLaunchKernelGGL((segment_sum_kernel<true, T>), grid, dim3(256), 0, (hipStream_t)stream, src,
                        rowptr, idx, row_scale, scale, n_rows, width, out);
   else
@@ -590,40 +646,68 @@ int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, 
   return check_launch("segment_order_bwd");
 }
 
-int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
-                 const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
-                 void* stream) {
+static int cgc_launch_fwd(const float* ps, const float* pr, const float* ep, const float* ef,
+                          const float* ea, const int* sender, const int* rowptr,
+                          const float* row_scale, int n_nodes, int D, float* agg, void* stream) {
   if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_fwd: D = %d > %d not built", D, EELG_CGC_MAXD);
-  if (D > 128)
-    hipLaunchKernelGGL(cgc_fwd_kernel<4>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
-  else if (D > 64)
-    hipLaunchKernelGGL(cgc_fwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
-  else
-    hipLaunchKernelGGL(cgc_fwd_kernel<1>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, agg);
+  const dim3 g((n_nodes + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define CGCF(C, E) hipLaunchKernelGGL((cgc_fwd_kernel<C, E>), g, dim3(256), 0, st, ps, pr, ep, ef, ea, \
+                                      sender, rowptr, row_scale, n_nodes, D, agg)
+  const int cpl = D > 128 ? 4 : D > 64 ? 2 : 1;
+  if (ef) { if (cpl == 4) CGCF(4, true); else if (cpl == 2) CGCF(2, true); else CGCF(1, true); }
+  else { if (cpl == 4) CGCF(4, false); else if (cpl == 2) CGCF(2, false); else CGCF(1, false); }
+#undef CGCF
   return check_launch("cgc_fwd");
+}
+
+static int cgc_launch_bwd(const float* ps, const float* pr, const float* ep, const float* ef,
+                          const float* ea, const int* sender, const int* rowptr,
+                          const float* row_scale, int n_nodes, int D, const float* grad_agg,
+                          float* dz, float* grad_pr, void* stream) {
+  if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
+  if (n_nodes <= 0) return 0;
+  if (D > EELG_CGC_MAXD) return fail(-2, "cgc_bwd: D = %d > %d not built", D, EELG_CGC_MAXD);
+  const dim3 g((n_nodes + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define CGCB(C, E) hipLaunchKernelGGL((cgc_bwd_kernel<C, E>), g, dim3(256), 0, st, ps, pr, ep, ef, ea, \
+                                      sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr)
+  const int cpl = D > 128 ? 4 : D > 64 ? 2 : 1;
+  if (ef) { if (cpl == 4) CGCB(4, true); else if (cpl == 2) CGCB(2, true); else CGCB(1, true); }
+  else { if (cpl == 4) CGCB(4, false); else if (cpl == 2) CGCB(2, false); else CGCB(1, false); }
+#undef CGCB
+  return check_launch("cgc_bwd");
+}
+
+int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
+                 const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
+                 void* stream) {
+  return cgc_launch_fwd(ps, pr, ep, nullptr, nullptr, sender, rowptr, row_scale, n_nodes, D, agg,
+                        stream);
 }
 
 int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D,
                  const float* grad_agg, float* dz, float* grad_pr, void* stream) {
-  if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
-  if (n_nodes <= 0) return 0;
-  if (D > EELG_CGC_MAXD) return fail(-2, "cgc_bwd: D = %d > %d not built", D, EELG_CGC_MAXD);
-  if (D > 128)
-    hipLaunchKernelGGL(cgc_bwd_kernel<4>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
-  else if (D > 64)
-    hipLaunchKernelGGL(cgc_bwd_kernel<2>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
-  else
-    hipLaunchKernelGGL(cgc_bwd_kernel<1>, dim3((n_nodes + 3) / 4), dim3(256), 0, (hipStream_t)stream, ps,
-                       pr, ep, sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr);
-  return check_launch("cgc_bwd");
+  return cgc_launch_bwd(ps, pr, ep, nullptr, nullptr, sender, rowptr, row_scale, n_nodes, D,
+                        grad_agg, dz, grad_pr, stream);
+}
+
+int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
+                    const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
+                    int D, float* agg, void* stream) {
+  if (!ef || !ea) return fail(-2, "cgc_fwd_ef: ef and ea are required");
+  return cgc_launch_fwd(ps, pr, nullptr, ef, ea, sender, rowptr, row_scale, n_nodes, D, agg, stream);
+}
+
+int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
+                    const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
+                    int D, const float* grad_agg, float* dz, float* grad_pr, void* stream) {
+  if (!ef || !ea) return fail(-2, "cgc_bwd_ef: ef and ea are required");
+  return cgc_launch_bwd(ps, pr, nullptr, ef, ea, sender, rowptr, row_scale, n_nodes, D, grad_agg,
+                        dz, grad_pr, stream);
 }
 
 int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_rows, const float* B,

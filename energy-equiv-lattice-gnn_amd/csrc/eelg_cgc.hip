@@ -11,6 +11,12 @@
 // [E, D] messages.  Edges are receiver-sorted (rowptr = receiver CSR): one wave per
 // receiver sums its in-edges in registers (no atomics).  softplus follows torch's
 // default (beta 1, threshold 20).
+//
+// Factored edge features (EF, the model path): in both reference models the edge features are
+// themselves a Linear of 5 per-edge inputs, f = e5 W5^T + b5 (cgc_modified.py:71-74), so
+// Ep = f W_e^T = [e5 | 1] A with A = [W5^T W_e^T ; b5 W_e^T] ([6, 2D], formed on the host per
+// layer).  With EF the kernels read the 8-float rows ef = [e5 | 1 | 0 | 0] (32 B per edge) and
+// the [8, 2D] A instead of the [E, 2D] Ep (1 KiB per edge at D = 128), and form Ep in registers.
 #include <hip/hip_runtime.h>
 
 __device__ __forceinline__ float cgc_softplus(float z) { return z > 20.0f ? z : log1pf(expf(z)); }
@@ -23,9 +29,51 @@ __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + ex
 #ifndef CGC_EB
 #define CGC_EB 4
 #endif
-template <int CPL>
+#define CGC_EFW 8   // floats per factored edge-feature row: e5, 1, two zeros
+#define CGC_EFN 6   // rows of A used
+template <int CPL, bool EF>
+__device__ __forceinline__ void cgc_edge_proj(const float* __restrict__ ep, const float* __restrict__ ef,
+                                              const float (&av)[CGC_EFN][CPL], const float (&am)[CGC_EFN][CPL],
+                                              int e, int D2, int D, int lane, float (&pv)[CPL], float (&pm)[CPL]) {
+  if (EF) {
+    float f[CGC_EFN];
+#pragma unroll
+    for (int i = 0; i < CGC_EFN; ++i) f[i] = ef[(size_t)e * CGC_EFW + i];   // wave-uniform
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      float v = 0.0f, m = 0.0f;
+#pragma unroll
+      for (int i = 0; i < CGC_EFN; ++i) { v = fmaf(f[i], av[i][k], v); m = fmaf(f[i], am[i][k], m); }
+      pv[k] = v;
+      pm[k] = m;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = min(lane + 64 * k, D - 1);
+      pv[k] = ep[(size_t)e * D2 + c];
+      pm[k] = ep[(size_t)e * D2 + D + c];
+    }
+  }
+}
+
+template <int CPL, bool EF>
+__device__ __forceinline__ void cgc_load_a(const float* __restrict__ ea, int D, int lane,
+                                           float (&av)[CGC_EFN][CPL], float (&am)[CGC_EFN][CPL]) {
+#pragma unroll
+  for (int i = 0; i < CGC_EFN; ++i)
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = min(lane + 64 * k, D - 1);
+      av[i][k] = EF ? ea[(size_t)i * 2 * D + c] : 0.0f;
+      am[i][k] = EF ? ea[(size_t)i * 2 * D + D + c] : 0.0f;
+    }
+}
+
+template <int CPL, bool EF>
 __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
+    const float* __restrict__ ef, const float* __restrict__ ea,
     const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, float* __restrict__ agg) {
   const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -36,6 +84,8 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
   const float sc = row_scale ? row_scale[node] : 1.0f;
   const float* __restrict__ prn = pr + (size_t)node * D2;
   float rv[CPL], rm[CPL], acc[CPL];
+  float av[CGC_EFN][CPL], am[CGC_EFN][CPL];
+  cgc_load_a<CPL, EF>(ea, D, lane, av, am);
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int c = min(lane + 64 * k, D - 1);
@@ -47,23 +97,24 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     int s[CGC_EB];
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j) s[j] = sender[min(e0 + j, end - 1)];
-    float zv[CGC_EB][CPL], zm[CGC_EB][CPL];
+    float zv[CGC_EB][CPL], zm[CGC_EB][CPL], pv[CGC_EB][CPL], pm[CGC_EB][CPL];
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j) {
       const int e = min(e0 + j, end - 1);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = min(lane + 64 * k, D - 1);
-        zv[j][k] = ps[(size_t)s[j] * D2 + c] + ep[(size_t)e * D2 + c];
-        zm[j][k] = ps[(size_t)s[j] * D2 + D + c] + ep[(size_t)e * D2 + D + c];
+        zv[j][k] = ps[(size_t)s[j] * D2 + c];
+        zm[j][k] = ps[(size_t)s[j] * D2 + D + c];
       }
+      cgc_edge_proj<CPL, EF>(ep, ef, av, am, e, D2, D, lane, pv[j], pm[j]);
     }
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j)
       if (e0 + j < end)   // uniform
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
-          acc[k] += cgc_softplus(zv[j][k] + rv[k]) * cgc_sigmoid(zm[j][k] + rm[k]);
+          acc[k] += cgc_softplus((zv[j][k] + pv[j][k]) + rv[k]) * cgc_sigmoid((zm[j][k] + pm[j][k]) + rm[k]);
   }
 #pragma unroll
   for (int k = 0; k < CPL; ++k)
@@ -75,10 +126,10 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
 // Gs (for dW_s and dx) are a segmented sum of dz over the sender CSR.  Edges are taken CGC_EB
 // at a time like the forward: the batch's sender indices are read together and every gather
 // of Ps[s] / Ep[e] is issued before any of them is used.
-template <int CPL>
+template <int CPL, bool EF>
 __global__ __launch_bounds__(256) void cgc_bwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
-    const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
+    const float* __restrict__ ef, const float* __restrict__ ea, const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, const float* __restrict__ gagg, float* __restrict__ dz, float* __restrict__ gr) {
   const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
@@ -88,6 +139,8 @@ __global__ __launch_bounds__(256) void cgc_bwd_kernel(
   const float sc = row_scale ? row_scale[node] : 1.0f;
   const float* __restrict__ prn = pr + (size_t)node * D2;
   float rv[CPL], rm[CPL], g[CPL], av[CPL], am[CPL];
+  float aav[CGC_EFN][CPL], aam[CGC_EFN][CPL];
+  cgc_load_a<CPL, EF>(ea, D, lane, aav, aam);
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int c = min(lane + 64 * k, D - 1);
@@ -101,23 +154,24 @@ __global__ __launch_bounds__(256) void cgc_bwd_kernel(
     int s[CGC_EB];
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j) s[j] = sender[min(e0 + j, end - 1)];
-    float zv[CGC_EB][CPL], zm[CGC_EB][CPL];
+    float zv[CGC_EB][CPL], zm[CGC_EB][CPL], pv[CGC_EB][CPL], pm[CGC_EB][CPL];
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j) {
       const int e = min(e0 + j, end - 1);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int c = min(lane + 64 * k, D - 1);
-        zv[j][k] = ps[(size_t)s[j] * D2 + c] + ep[(size_t)e * D2 + c];
-        zm[j][k] = ps[(size_t)s[j] * D2 + D + c] + ep[(size_t)e * D2 + D + c];
+        zv[j][k] = ps[(size_t)s[j] * D2 + c];
+        zm[j][k] = ps[(size_t)s[j] * D2 + D + c];
       }
+      cgc_edge_proj<CPL, EF>(ep, ef, aav, aam, e, D2, D, lane, pv[j], pm[j]);
     }
 #pragma unroll
     for (int j = 0; j < CGC_EB; ++j)
       if (e0 + j < end)   // uniform
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-          const float z1 = zv[j][k] + rv[k], z2 = zm[j][k] + rm[k];
+          const float z1 = (zv[j][k] + pv[j][k]) + rv[k], z2 = (zm[j][k] + pm[j][k]) + rm[k];
           const float sv = z1 > 20.0f ? 1.0f : cgc_sigmoid(z1);   // softplus' (torch: 1 above threshold)
           const float sm = cgc_sigmoid(z2);
           const float dv = g[k] * sv * sm;

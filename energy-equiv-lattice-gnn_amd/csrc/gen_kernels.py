@@ -78,6 +78,24 @@ SC_NT = int(os.environ.get("EELG_SC_NT", "1"))
 # (and one pinned SGPR, hence an s_mov_b32 per term) per coefficient.  r04f kbench: fwd 0.312 vs
 # 0.326 ms, grad-x 0.349 vs 0.357
 SC_CVEC = int(os.environ.get("EELG_SC_CVEC", "1"))
+# fwd / grad-x packed: two nodes per lane (lane, lane + 64 of a 128-node tile) on v_pk_fma_f32,
+# each coefficient broadcast from ONE half of an aligned SGPR pair by op_sel / op_sel_hi (inline
+# asm: the compiler builds (c, c) pairs with an s_mov per odd coefficient instead).  Round-5
+# microbenchmark (tools/proto/valu_ceiling.hip, profiles/r05b_valu.txt): a plain v_fmac_f32 with
+# an SGPR operand issues once per ~4 cycles per SIMD at ANY occupancy (77 TFLOP/s), all-VGPR
+# FMAs reach 118-120 TF and the op_sel-broadcast packed FMA 132-140 TF at 2-4 waves per SIMD
+SC_PK = int(os.environ.get("EELG_SC_PK", "1"))
+# packed grad-x: 32-term blocks (64 with one block ahead spills SGPRs once the volatile packed
+# statements fix the order)
+SC_PK_BLOCK_BWD = int(os.environ.get("EELG_SC_PK_BLOCK_BWD", "32"))
+# packed: 1 = every packed statement a volatile asm in the _PkSched order; 0 = the broadcast FMAs
+# as plain asm and the VGPR products / FMAs as vector C++, in term order, scheduled by the compiler
+SC_PK_SCHED = int(os.environ.get("EELG_SC_PK_SCHED", "1"))
+# packed coefficient operands: "asm" = one aligned SGPR pair per two terms, the odd term broadcast
+# by op_sel in inline asm; "dual" = each block scalar-loaded twice (at t0 and t0 + 1), so every
+# coefficient is the LOW half of an aligned pair, which the compiler broadcasts by itself
+# (op_sel_hi:[0,..]) -- no inline asm, no hazard s_nops, twice the SGPRs per block
+SC_PK_MODE = os.environ.get("EELG_SC_PK_MODE", "asm")
 # coefficient gradient: LDS-resident nodes per workgroup, waves per workgroup, the most
 # accumulators (terms) per wave
 SC_COEF_CHUNK = int(os.environ.get("EELG_SC_COEF_CHUNK", "512"))
@@ -925,6 +943,353 @@ def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> L
     return out
 
 
+def _pk_cload(blk, CE):
+    if SC_PK_MODE == "dual":
+        return _pk_cload_dual(blk, CE)
+    if SC_PK_MODE == "pairs":
+        return _pk_cload_pairs(blk, CE)
+    return _pk_cload_asm(blk, CE)
+
+
+def _pk_cload_pairs(blk, CE):
+    """One 8-byte scalar load per coefficient, at its own offset: the coefficient is the low
+    half of its own aligned SGPR pair (the compiler merges neighbouring loads into wider ones)
+    and only pairs are pinned, never whole vectors"""
+    ts = blk["terms"]
+    out, names = [], []
+    for t in ts:
+        nm = f"cp{t}"
+        out.append(f"  eelg_c2 {nm} = *reinterpret_cast<const eelg_c2*>(cf + {t});")
+        CE[t] = (f"eelg_splat({nm}, 0)", 0)
+        names.append(nm)
+    return out, names
+
+
+def _pk_cload_dual(blk, CE):
+    """Two scalar-load sets of a block's coefficients, at t0 and at t0 + 1 (16 / 8 / 4 / 2 terms
+    per load; rows are padded past the last term): term t0 + i is element i of the first set for
+    even i and element i - 1 of the second for odd i, always an even element, i.e. the low half
+    of an aligned SGPR pair.  CE[t] = the splat expression."""
+    ts = blk["terms"]
+    t0, n = ts[0], len(ts)
+    assert ts == list(range(t0, t0 + n))
+    out, names = [], []
+    for sh, tag in ((0, "a"), (1, "b")):
+        t = t0 + sh
+        cnt = n - sh
+        while cnt > 0:
+            sz = next(z for z in (16, 8, 4, 2) if z <= max(cnt, 2))
+            nm = f"cv{tag}{t}"
+            out.append(f"  eelg_c{sz} {nm} = *reinterpret_cast<const eelg_c{sz}*>(cf + {t});")
+            for i in range(0, min(sz, cnt), 2):
+                CE[t + i] = (f"eelg_splat({nm}, {i})", 0)
+            names.append(nm)
+            t += sz
+            cnt -= sz
+    return out, names
+
+
+def _pk_cload_asm(blk, CE):
+    """Scalar loads of a block's coefficients as SGPR vectors of 16 / 8 / 4 / 2 terms (an odd tail
+    is loaded as a pair: the row is padded past the last term).  CE[t] = (pair expression, half):
+    the aligned SGPR pair holding coefficient t, and which half of it (op_sel)."""
+    ts = blk["terms"]
+    t0, n = ts[0], len(ts)
+    assert ts == list(range(t0, t0 + n))
+    out, names, t = [], [], t0
+    while t < t0 + n:
+        left = t0 + n - t
+        sz = next(z for z in (16, 8, 4, 2) if z <= max(left, 2))
+        nm = f"cv{t}"
+        out.append(f"  eelg_c{sz} {nm} = *reinterpret_cast<const eelg_c{sz}*>(cf + {t});")
+        for i in range(min(sz, left)):
+            CE[t + i] = (f"eelg_pair({nm}, {i // 2})" if sz > 2 else nm, i % 2)
+        names.append(nm)
+        t += sz
+    return out, names
+
+
+class _PkSched:
+    """The packed VALU stream of one coefficient block as a list of instructions (macro text,
+    written variables, read variables), emitted as ``asm volatile`` in a dependency-respecting
+    order that keeps every consumer at least one instruction behind its producer.  The hazard
+    recognizer puts an ``s_nop`` before an inline-asm reader of a VGPR that one of the two
+    preceding VALU instructions wrote (2857 / 5801 of them in sc_fwd / sc_bwd_x of sc_l4_c3
+    before this order),
+    and the compiler's scheduler places products right before their first use; a fixed order of
+    volatile statements leaves it nothing to undo.  A small look-ahead window bounds the register
+    live ranges."""
+
+    def __init__(self, window=10, dist=2):
+        self.ins = []
+        self.window = window
+        self.dist = dist            # keep a reader at least this many instructions behind
+
+    def add(self, text, writes, reads):
+        self.ins.append((text, tuple(writes), tuple(reads)))
+
+    def emit(self, ind="  "):
+        n = len(self.ins)
+        if not SC_PK_SCHED:
+            out = [ind + t for t, _, _ in self.ins]
+            self.ins = []
+            return out
+        deps = [set() for _ in range(n)]
+        last_w, reads_since = {}, {}
+        for j, (_, w, r) in enumerate(self.ins):
+            for v in r:
+                if v in last_w:
+                    deps[j].add(last_w[v])              # RAW
+            for v in w:
+                if v in last_w:
+                    deps[j].add(last_w[v])              # WAW
+                for i in reads_since.get(v, ()):
+                    if i != j:
+                        deps[j].add(i)                  # WAR
+            for v in r:
+                reads_since.setdefault(v, []).append(j)
+            for v in w:
+                last_w[v] = j
+                reads_since[v] = []
+        done, out, recent = [False] * n, [], []
+        pending = list(range(n))
+        while pending:
+            pick, best = None, None
+            for j in pending[: self.window]:
+                if all(done[i] for i in deps[j]):
+                    # distance to the nearest recent producer of an operand (0 = none recent)
+                    near = next((k for k, w in enumerate(reversed(recent), 1)
+                                 if set(self.ins[j][2]) & set(w)), 0)
+                    if near == 0:
+                        pick = j
+                        break
+                    if best is None or near > best:
+                        pick, best = j, near
+            j = pick
+            done[j] = True
+            pending.remove(j)
+            out.append(ind + self.ins[j][0])
+            recent = (recent + [self.ins[j][1]])[-self.dist:]
+        self.ins = []
+        return out
+
+
+def emit_sc_packed(L, name, plan, lin, lout, D, Dout, TP, NB, NTH, head, stage_in, stage_out,
+                   cm_store, lq):
+    """sc_fwd / sc_bwd_x with two nodes per lane (tile rows lane and lane + 64) on packed fp32:
+    every coefficient FMA is one v_pk_fma_f32 whose SGPR operand broadcasts one half of an aligned
+    coefficient pair (EELG_PKF_LO / _HI), the pair / triple products and the grad-x chain are
+    v_pk_mul_f32 / v_pk_fma_f32 on VGPRs (EELG_PKMV / EELG_PKFV), all scheduled by _PkSched.
+    Same blocks, prefetch and pins as the plain form."""
+    CE = {}
+    S = _PkSched()
+
+    def cfma(t, b, c):
+        pr, hf = CE[t]
+        if SC_PK_MODE in ("dual", "pairs"):
+            S.add(f"{c} = __builtin_elementwise_fma({pr}, {b}, {c});", [c], [c, b])
+        else:
+            S.add(f"EELG_PKF_{'HI' if hf else 'LO'}({c}, {pr}, {b});", [c], [c, b])
+
+    def cmul(t, b, c):
+        pr, hf = CE[t]
+        if SC_PK_MODE in ("dual", "pairs"):
+            S.add(f"{c} = __builtin_elementwise_fma({pr}, {b}, (eelg_f2r){{0.0f, 0.0f}});", [c], [b])
+        else:
+            S.add(f"EELG_PKM_{'HI' if hf else 'LO'}({c}, {pr}, {b});", [c], [b])
+
+    def vmul(d, a, b):
+        S.add(f"EELG_PKMV({d}, {a}, {b});", [d], [a, b])
+
+    def vfma(d, a, b):
+        S.add(f"EELG_PKFV({d}, {a}, {b});", [d], [d, a, b])
+
+    rows = [f"  float* __restrict__ tr0 = tile + lane * {TP};",
+            f"  float* __restrict__ tr1 = tile + (lane + 64) * {TP};"]
+
+    def ld2(col):
+        return f"(eelg_f2r){{tr0[{col}], tr1[{col}]}}"
+
+    # ---------------- forward ----------------
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
+    L.append("    float* __restrict__ out) {")
+    L.append(f"  __shared__ float tile[{NB} * {TP}];")
+    L += head
+    L += stage_in("x", "tile", lin, NB, NTH)
+    L.append("  __syncthreads();")
+    L += rows
+    for a in range(D):
+        L.append(f"  eelg_f2r x{a} = {ld2(lq(lin, a, 'cl'))};")
+    blocks = sc_blocks(plan, SC_BLOCK_FWD)
+    fv = [f"x{a}" for a in range(D)]
+    pf = {}
+    for j in range(min(SC_PFD_FWD, len(blocks))):
+        lines, pf[j] = _pk_cload(blocks[j], CE)
+        L += lines
+    declared = set()
+    for q in range(Dout):
+        L.append(f"  eelg_f2r o{q};")
+
+    def acc(t, q, b):
+        # the first term into o_q is a multiply (no zero fill of the accumulators)
+        if q in declared:
+            cfma(t, b, f"o{q}")
+        else:
+            cmul(t, b, f"o{q}")
+            declared.add(q)
+    pdecl = set()
+    for bi, blk in enumerate(blocks):
+        if bi + SC_PFD_FWD < len(blocks):
+            lines, pf[bi + SC_PFD_FWD] = _pk_cload(blocks[bi + SC_PFD_FWD], CE)
+            L += lines
+        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_FWD) for nm in pf.get(j, [])]
+        carry = []
+        tmp = []
+        if blk["kind"] == "deg1":
+            for t, a, q in blk["deg1"]:
+                acc(t, q, f"x{a}")
+        for sg in blk.get("segs", []):
+            a, b = sg["a"], sg["b"]
+            pv = f"p{a}_{b}"
+            if sg["first"]:
+                pdecl.add(pv)
+                L.append(f"  eelg_f2r {pv};")
+                vmul(pv, f"x{a}", f"x{b}")
+            for t, q in sg["d2"]:
+                acc(t, q, pv)
+            for cc, lst in sg["d3"]:
+                mv = f"m{a}_{b}_{cc}"
+                tmp.append(mv)
+                vmul(mv, pv, f"x{cc}")
+                for t, q in lst:
+                    acc(t, q, mv)
+            if not sg["last"]:
+                carry = [pv]
+        if tmp:
+            L.append("  eelg_f2r " + ", ".join(tmp) + ";")
+        L.append("  {")
+        L += S.emit("    ")
+        L.append("  }")
+        L.append("  " + pin(fv + sorted(f"o{q}" for q in declared) + carry, sgprs=nxt))
+    for q in range(Dout):
+        if q not in declared:
+            L.append(f"  o{q} = (eelg_f2r){{0.0f, 0.0f}};")
+    L.append("  __syncthreads();")
+    for q in range(Dout):
+        col = lq(lout, q, 'cl')
+        L.append(f"  tr0[{col}] = o{q}.x; tr1[{col}] = o{q}.y;")
+    L.append("  __syncthreads();")
+    L += stage_out("out", "tile", lout, NB, NTH)
+    L.append("}")
+
+    # ---------------- backward w.r.t. x ----------------
+    CE.clear()
+    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
+    L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
+    L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
+    L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
+    L.append(f"  __shared__ float tile[{NB} * {TP}];")
+    L += head
+    L += stage_in("x", "tile", lin, NB, NTH)
+    L.append("  __syncthreads();")
+    L.append("  if (xt) {")
+    L += cm_store("xt", "tile", lin, NB, "    ", NTH)
+    L.append("  }")
+    L += rows
+    for a in range(D):
+        L.append(f"  eelg_f2r x{a} = {ld2(lq(lin, a, 'cl'))};")
+    L.append("  __syncthreads();")
+    L += stage_in("gout", "tile", lout, NB, NTH)
+    L.append("  __syncthreads();")
+    L.append("  if (gt) {")
+    L += cm_store("gt", "tile", lout, NB, "    ", NTH)
+    L.append("  }")
+    for q in range(Dout):
+        L.append(f"  eelg_f2r g{q} = {ld2(lq(lout, q, 'cl'))};")
+    dset = set()
+    for a in range(D):
+        L.append(f"  eelg_f2r d{a};")
+    blocks = sc_blocks(plan, SC_PK_BLOCK_BWD)
+    pf = {}
+    for j in range(min(SC_PFD_BWD, len(blocks))):
+        lines, pf[j] = _pk_cload(blocks[j], CE)
+        L += lines
+
+    def dacc(a, u, v):
+        """d_a += u * v (the first contribution a multiply)"""
+        if a in dset:
+            vfma(f"d{a}", u, v)
+        else:
+            vmul(f"d{a}", u, v)
+            dset.add(a)
+    for bi, blk in enumerate(blocks):
+        if bi + SC_PFD_BWD < len(blocks):
+            lines, pf[bi + SC_PFD_BWD] = _pk_cload(blocks[bi + SC_PFD_BWD], CE)
+            L += lines
+        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_BWD) for nm in pf.get(j, [])]
+        carry = []
+        tmp = []
+        if blk["kind"] == "deg1":
+            for t, a, q in blk["deg1"]:
+                if a in dset:
+                    cfma(t, f"g{q}", f"d{a}")
+                else:
+                    cmul(t, f"g{q}", f"d{a}")
+                    dset.add(a)
+        for sg in blk.get("segs", []):
+            a, b = sg["a"], sg["b"]
+            pv, sv = f"p{a}_{b}", f"s{a}_{b}"
+            first_sv = True
+            if sg["first"]:
+                L.append(f"  eelg_f2r {pv}, {sv};")
+                vmul(pv, f"x{a}", f"x{b}")
+            else:
+                first_sv = False                      # carried in from the previous block
+            for t, q in sg["d2"]:
+                if first_sv:
+                    cmul(t, f"g{q}", sv)
+                    first_sv = False
+                else:
+                    cfma(t, f"g{q}", sv)
+            for cc, lst in sg["d3"]:
+                s = f"s{a}_{b}_{cc}"
+                tmp.append(s)
+                for k, (t, q) in enumerate(lst):
+                    (cmul if k == 0 else cfma)(t, f"g{q}", s)
+                dacc(cc, s, pv)
+                if first_sv:
+                    vmul(sv, s, f"x{cc}")
+                    first_sv = False
+                else:
+                    vfma(sv, s, f"x{cc}")
+            if sg["last"]:
+                if first_sv:
+                    raise AssertionError("a pair segment with no terms")
+                dacc(a, sv, f"x{b}")
+                dacc(b, sv, f"x{a}")
+            else:
+                carry = [pv, sv]
+        if tmp:
+            L.append("  eelg_f2r " + ", ".join(tmp) + ";")
+        L.append("  {")
+        L += S.emit("    ")
+        L.append("  }")
+        bv = ([f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] +
+              sorted(f"d{a}" for a in dset))
+        L.append("  " + pin(bv + carry, sgprs=nxt))
+    for a in range(D):
+        if a not in dset:
+            L.append(f"  d{a} = (eelg_f2r){{0.0f, 0.0f}};")
+    L.append("  __syncthreads();")
+    for a in range(D):
+        col = lq(lin, a, 'cl')
+        L.append(f"  tr0[{col}] = d{a}.x; tr1[{col}] = d{a}.y;")
+    L.append("  __syncthreads();")
+    L += stage_out("gx", "tile", lin, NB, NTH)
+    L.append("}")
+
+
 def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[str, dict]:
     """Symmetric contraction kernels.
 
@@ -964,7 +1329,9 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
         TP += 1                             # odd -> conflict-free lane rows
     drow, orow = lin.row, lout.row
     nt = len(plan.terms)
-    cld = -(-nt // 16) * 16                  # coefficient row stride: 64-B aligned channel rows
+    # coefficient row stride: 64-B aligned channel rows, at least one float past the last term (the
+    # packed kernels load coefficients in pairs)
+    cld = -(-(nt + (1 if SC_PK else 0)) // 16) * 16
 
     def lq(lay, a, cl):
         """LDS column of component a for channel-in-quad cl (may be a runtime expr)."""
@@ -986,7 +1353,7 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     if lout.comp == lin.comp:
         lout.goff = lin.goff
 
-    NB = 64 * SC_NT                         # nodes per workgroup (fwd / grad-x), one per lane
+    NB = 128 if SC_PK else 64 * SC_NT        # nodes per workgroup (fwd / grad-x): one (two packed) per lane
     NTH = 256 * SC_NT                       # threads per workgroup (fwd / grad-x)
     VT = "float"
 
@@ -1134,124 +1501,128 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
             f"  const int cl = __builtin_amdgcn_readfirstlane(wv & {Q - 1});",
             f"  const float* __restrict__ cf = coef + (size_t)c * {cld};"]
 
-    # ---------------- forward ----------------
-    L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
-    L.append("    float* __restrict__ out) {")
-    L.append(f"  __shared__ float tile[{NB} * {TP}];")
-    L += head
-    L += stage_in("x", "tile", lin, NB, NTH)
-    L.append("  __syncthreads();")
-    L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
-    for a in range(D):
-        L.append(f"  {VT} x{a} = {lds_get('tr', lq(lin, a, 'cl'))};")
-    for q in range(Dout):
-        L.append(f"  {VT} o{q} = {zero};")
-    blocks = sc_blocks(plan, SC_BLOCK_FWD)
-    fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
-    pf = {}
-    for j in range(min(SC_PFD_FWD, len(blocks))):
-        lines, pf[j] = cload(blocks[j])
-        L += lines
-    for bi, blk in enumerate(blocks):
-        # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
-        if bi + SC_PFD_FWD < len(blocks):
-            lines, pf[bi + SC_PFD_FWD] = cload(blocks[bi + SC_PFD_FWD])
+    if SC_PK:
+        emit_sc_packed(L, name, plan, lin, lout, D, Dout, TP, NB, NTH, head, stage_in, stage_out,
+                       cm_store, lq)
+    else:
+        # ---------------- forward ----------------
+        L.append(f"__global__ __launch_bounds__({NTH}) void sc_fwd_{name}(")
+        L.append("    const float* __restrict__ x, const float* __restrict__ coef, int n_nodes,")
+        L.append("    float* __restrict__ out) {")
+        L.append(f"  __shared__ float tile[{NB} * {TP}];")
+        L += head
+        L += stage_in("x", "tile", lin, NB, NTH)
+        L.append("  __syncthreads();")
+        L.append(f"  float* __restrict__ tr = tile + {nrow} * {TP};")
+        for a in range(D):
+            L.append(f"  {VT} x{a} = {lds_get('tr', lq(lin, a, 'cl'))};")
+        for q in range(Dout):
+            L.append(f"  {VT} o{q} = {zero};")
+        blocks = sc_blocks(plan, SC_BLOCK_FWD)
+        fv = [f"x{a}" for a in range(D)] + [f"o{q}" for q in range(Dout)]
+        pf = {}
+        for j in range(min(SC_PFD_FWD, len(blocks))):
+            lines, pf[j] = cload(blocks[j])
             L += lines
-        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_FWD) for nm in pf.get(j, [])]
-        carry = []
-        if blk["kind"] == "deg1":
-            for t, a, q in blk["deg1"]:
-                L.append(f"  o{q} = {cfma(t, f'x{a}', f'o{q}')};")
-        for sg in blk.get("segs", []):
-            a, b = sg["a"], sg["b"]
-            pv = f"p{a}_{b}"
-            if sg["first"]:
-                L.append(f"  {VT} {pv} = x{a} * x{b};")
-            for t, q in sg["d2"]:
-                L.append(f"  o{q} = {cfma(t, pv, f'o{q}')};")
-            for cc, lst in sg["d3"]:
-                L.append(f"  {{ const {VT} m = {pv} * x{cc};")
-                for t, q in lst:
-                    L.append(f"    o{q} = {cfma(t, 'm', f'o{q}')};")
-                L.append("  }")
-            if not sg["last"]:
-                carry = [pv]
-        L.append("  " + pin(fv + carry, sgprs=nxt))
-    L.append("  __syncthreads();")
-    for q in range(Dout):
-        L.append(f"  {lds_put('tr', lq(lout, q, 'cl'), f'o{q}')}")
-    L.append("  __syncthreads();")
-    L += stage_out("out", "tile", lout, NB, NTH)
-    L.append("}")
+        for bi, blk in enumerate(blocks):
+            # coefficients SC_PFD_FWD blocks ahead are in flight (scalar loads) while this block computes
+            if bi + SC_PFD_FWD < len(blocks):
+                lines, pf[bi + SC_PFD_FWD] = cload(blocks[bi + SC_PFD_FWD])
+                L += lines
+            nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_FWD) for nm in pf.get(j, [])]
+            carry = []
+            if blk["kind"] == "deg1":
+                for t, a, q in blk["deg1"]:
+                    L.append(f"  o{q} = {cfma(t, f'x{a}', f'o{q}')};")
+            for sg in blk.get("segs", []):
+                a, b = sg["a"], sg["b"]
+                pv = f"p{a}_{b}"
+                if sg["first"]:
+                    L.append(f"  {VT} {pv} = x{a} * x{b};")
+                for t, q in sg["d2"]:
+                    L.append(f"  o{q} = {cfma(t, pv, f'o{q}')};")
+                for cc, lst in sg["d3"]:
+                    L.append(f"  {{ const {VT} m = {pv} * x{cc};")
+                    for t, q in lst:
+                        L.append(f"    o{q} = {cfma(t, 'm', f'o{q}')};")
+                    L.append("  }")
+                if not sg["last"]:
+                    carry = [pv]
+            L.append("  " + pin(fv + carry, sgprs=nxt))
+        L.append("  __syncthreads();")
+        for q in range(Dout):
+            L.append(f"  {lds_put('tr', lq(lout, q, 'cl'), f'o{q}')}")
+        L.append("  __syncthreads();")
+        L += stage_out("out", "tile", lout, NB, NTH)
+        L.append("}")
 
 
-    # ---------------- backward w.r.t. x ----------------
-    L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
-    L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
-    L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
-    L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
-    # one LDS tile, used three times (x in, grad_out in, grad_x out): 2x the occupancy of
-    # separate x / grad_out tiles.  When xt / gt are given, the staged tiles are also written
-    # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
-    L.append(f"  __shared__ float tx[{NB} * {TP}];")
-    L += head
-    L += stage_in("x", "tx", lin, NB, NTH)
-    L.append("  __syncthreads();")
-    L.append("  if (xt) {")
-    L += cm_store("xt", "tx", lin, NB, "    ", NTH)
-    L.append("  }")
-    L.append(f"  float* __restrict__ xr = tx + {nrow} * {TP};")
-    for a in range(D):
-        L.append(f"  {VT} x{a} = {lds_get('xr', lq(lin, a, 'cl'))};")
-        L.append(f"  {VT} d{a} = {zero};")
-    L.append("  __syncthreads();")
-    L += stage_in("gout", "tx", lout, NB, NTH)
-    L.append("  __syncthreads();")
-    L.append("  if (gt) {")
-    L += cm_store("gt", "tx", lout, NB, "    ", NTH)
-    L.append("  }")
-    for q in range(Dout):
-        L.append(f"  {VT} g{q} = {lds_get('xr', lq(lout, q, 'cl'))};")
-    bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
-    blocks = sc_blocks(plan, SC_BLOCK_BWD)
-    pf = {}
-    for j in range(min(SC_PFD_BWD, len(blocks))):
-        lines, pf[j] = cload(blocks[j])
-        L += lines
-    for bi, blk in enumerate(blocks):
-        # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
-        if bi + SC_PFD_BWD < len(blocks):
-            lines, pf[bi + SC_PFD_BWD] = cload(blocks[bi + SC_PFD_BWD])
+        # ---------------- backward w.r.t. x ----------------
+        L.append(f"__global__ __launch_bounds__({NTH}) void sc_bwd_x_{name}(")
+        L.append("    const float* __restrict__ x, const float* __restrict__ coef,")
+        L.append("    const float* __restrict__ gout, int n_nodes, float* __restrict__ gx,")
+        L.append("    float* __restrict__ xt, float* __restrict__ gt) {")
+        # one LDS tile, used three times (x in, grad_out in, grad_x out): 2x the occupancy of
+        # separate x / grad_out tiles.  When xt / gt are given, the staged tiles are also written
+        # channel-major (the coefficient gradient's operands) -- no separate transpose pass.
+        L.append(f"  __shared__ float tx[{NB} * {TP}];")
+        L += head
+        L += stage_in("x", "tx", lin, NB, NTH)
+        L.append("  __syncthreads();")
+        L.append("  if (xt) {")
+        L += cm_store("xt", "tx", lin, NB, "    ", NTH)
+        L.append("  }")
+        L.append(f"  float* __restrict__ xr = tx + {nrow} * {TP};")
+        for a in range(D):
+            L.append(f"  {VT} x{a} = {lds_get('xr', lq(lin, a, 'cl'))};")
+            L.append(f"  {VT} d{a} = {zero};")
+        L.append("  __syncthreads();")
+        L += stage_in("gout", "tx", lout, NB, NTH)
+        L.append("  __syncthreads();")
+        L.append("  if (gt) {")
+        L += cm_store("gt", "tx", lout, NB, "    ", NTH)
+        L.append("  }")
+        for q in range(Dout):
+            L.append(f"  {VT} g{q} = {lds_get('xr', lq(lout, q, 'cl'))};")
+        bv = [f"x{a}" for a in range(D)] + [f"g{q}" for q in range(Dout)] + [f"d{a}" for a in range(D)]
+        blocks = sc_blocks(plan, SC_BLOCK_BWD)
+        pf = {}
+        for j in range(min(SC_PFD_BWD, len(blocks))):
+            lines, pf[j] = cload(blocks[j])
             L += lines
-        nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_BWD) for nm in pf.get(j, [])]
-        carry = []
-        if blk["kind"] == "deg1":
-            for t, a, q in blk["deg1"]:
-                L.append(f"  d{a} = {cfma(t, f'g{q}', f'd{a}')};")
-        for sg in blk.get("segs", []):
-            a, b = sg["a"], sg["b"]
-            pv, sv = f"p{a}_{b}", f"s{a}_{b}"
-            if sg["first"]:
-                L.append(f"  {VT} {pv} = x{a} * x{b}; {VT} {sv} = {zero};")
-            for t, q in sg["d2"]:
-                L.append(f"  {sv} = {cfma(t, f'g{q}', sv)};")
-            for cc, lst in sg["d3"]:
-                L.append(f"  {{ {VT} s = {zero};")
-                for t, q in lst:
-                    L.append(f"    s = {cfma(t, f'g{q}', 's')};")
-                L.append(f"    d{cc} = {vfma('s', pv, f'd{cc}')}; {sv} = {vfma('s', f'x{cc}', sv)}; }}")
-            if sg["last"]:
-                L.append(f"  d{a} = {vfma(sv, f'x{b}', f'd{a}')}; d{b} = {vfma(sv, f'x{a}', f'd{b}')};")
-            else:
-                carry = [pv, sv]
-        L.append("  " + pin(bv + carry, sgprs=nxt))
-    L.append("  __syncthreads();")
-    for a in range(D):
-        L.append(f"  {lds_put('xr', lq(lin, a, 'cl'), f'd{a}')}")
-    L.append("  __syncthreads();")
-    L += stage_out("gx", "tx", lin, NB, NTH)
-    L.append("}")
+        for bi, blk in enumerate(blocks):
+            # coefficients SC_PFD_BWD blocks ahead are in flight (scalar loads) while this block computes
+            if bi + SC_PFD_BWD < len(blocks):
+                lines, pf[bi + SC_PFD_BWD] = cload(blocks[bi + SC_PFD_BWD])
+                L += lines
+            nxt = [nm for j in range(bi + 1, bi + 1 + SC_PFD_BWD) for nm in pf.get(j, [])]
+            carry = []
+            if blk["kind"] == "deg1":
+                for t, a, q in blk["deg1"]:
+                    L.append(f"  d{a} = {cfma(t, f'g{q}', f'd{a}')};")
+            for sg in blk.get("segs", []):
+                a, b = sg["a"], sg["b"]
+                pv, sv = f"p{a}_{b}", f"s{a}_{b}"
+                if sg["first"]:
+                    L.append(f"  {VT} {pv} = x{a} * x{b}; {VT} {sv} = {zero};")
+                for t, q in sg["d2"]:
+                    L.append(f"  {sv} = {cfma(t, f'g{q}', sv)};")
+                for cc, lst in sg["d3"]:
+                    L.append(f"  {{ {VT} s = {zero};")
+                    for t, q in lst:
+                        L.append(f"    s = {cfma(t, f'g{q}', 's')};")
+                    L.append(f"    d{cc} = {vfma('s', pv, f'd{cc}')}; {sv} = {vfma('s', f'x{cc}', sv)}; }}")
+                if sg["last"]:
+                    L.append(f"  d{a} = {vfma(sv, f'x{b}', f'd{a}')}; d{b} = {vfma(sv, f'x{a}', f'd{b}')};")
+                else:
+                    carry = [pv, sv]
+            L.append("  " + pin(bv + carry, sgprs=nxt))
+        L.append("  __syncthreads();")
+        for a in range(D):
+            L.append(f"  {lds_put('xr', lq(lin, a, 'cl'), f'd{a}')}")
+        L.append("  __syncthreads();")
+        L += stage_out("gx", "tx", lin, NB, NTH)
+        L.append("}")
 
     # ---------------- mul-major -> channel-major transpose ----------------
     # dst[(c * D + a) * n_nodes + n] = src[n, a-th component of channel c]; one kernel per
@@ -1417,6 +1788,8 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
 # ---------------------------------------------------------------------------
 def main(outdir: str) -> None:
     os.makedirs(outdir, exist_ok=True)
+    global _PKV
+    _PKV = "volatile" if SC_PK_SCHED else ""
     parts = ["// GENERATED by csrc/gen_kernels.py -- do not edit", "#include <hip/hip_runtime.h>",
              "#include <stdint.h>", '#include "../eelg_internal.h"', "",
              "// dword-aligned vector types: per-lane runs of d floats start at 4-byte boundaries",
@@ -1430,7 +1803,25 @@ def main(outdir: str) -> None:
              "typedef float eelg_c4 __attribute__((ext_vector_type(4), aligned(4)));",
              "typedef float eelg_c8 __attribute__((ext_vector_type(8), aligned(4)));",
              "typedef float eelg_c16 __attribute__((ext_vector_type(16), aligned(4)));",
-             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));", ""]
+             "typedef float eelg_f2r __attribute__((ext_vector_type(2)));",
+             "// packed contraction: acc (two nodes) += / = coefficient x b, the coefficient broadcast from",
+             "// the low / high half of an aligned SGPR pair by op_sel / op_sel_hi",
+             f'#define EELG_PKF_LO(acc, cp, b) asm {_PKV}("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(cp), "v"(b))',
+             f'#define EELG_PKF_HI(acc, cp, b) asm {_PKV}("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(cp), "v"(b))',
+             # the first term of a sum: an FMA onto the inline constant 0, not a v_pk_mul with op_sel
+             # (a VOP3P multiply with a broadcast operand costs its reader an s_nop)
+             f'#define EELG_PKM_LO(acc, cp, b) asm {_PKV}("v_pk_fma_f32 %0, %1, %2, 0 op_sel_hi:[0,1,1]" : "=v"(acc) : "s"(cp), "v"(b))',
+             f'#define EELG_PKM_HI(acc, cp, b) asm {_PKV}("v_pk_fma_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "=v"(acc) : "s"(cp), "v"(b))',
+             ('#define EELG_PKMV(d, a, b) asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b))'
+              if SC_PK_SCHED else '#define EELG_PKMV(d, a, b) ((d) = (a) * (b))'),
+             ('#define EELG_PKFV(d, a, b) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b))'
+              if SC_PK_SCHED else '#define EELG_PKFV(d, a, b) ((d) = __builtin_elementwise_fma((a), (b), (d)))'),
+             "template <typename V> __device__ __forceinline__ eelg_f2r eelg_splat(V v, int i) {",
+             "  return (eelg_f2r){v[i], v[i]};",
+             "}",
+             "template <typename V> __device__ __forceinline__ eelg_f2r eelg_pair(V v, int j) {",
+             "  return (eelg_f2r){v[2 * j], v[2 * j + 1]};",
+             "}", ""]
     for lmax in kernel_sets.LMAX:
         parts.append(emit_sh(lmax))
     # the row a tp_fwd stream reads for an edge past its range (also when the batch has no

@@ -7,8 +7,10 @@ keep the reference's parameter names.  The edge convolution
 ``eelg_cgc_bwd``): the [E, 3D] concatenation is never formed (the linear map is split
 into node-level projections gathered per edge plus one edge-level GEMM) and the
 scatter-add is a register sum per receiver over the receiver-sorted CSR shared with
-EnergyEquivGNN.  Weight gradients that reduce over nodes / edges use the split-K form
-(``ops._wgrad``).
+EnergyEquivGNN.  Every Linear of the models (node / edge projections, their gradients, the MLP head) runs on the
+in-tree MFMA linear kernels (``gnn/dense.py``); in the models the edge features enter in
+factored form (``eelg_cgc_fwd_ef``: the edge embedding composed with each layer's edge block), so
+the [E, 2D] edge projection is never written.
 """
 from __future__ import annotations
 
@@ -17,7 +19,7 @@ from typing import Dict, Optional
 
 import torch
 
-from . import _lib, ops
+from . import _lib, dense, ops
 from .blocks import EdgeIndex, as_csr
 
 # Mandel 6x6 from the 21 upper-triangular outputs (cgc_modified.py:28-33)
@@ -29,19 +31,34 @@ INDS_VAL = [[0, 1, 2, 3, 4, 5],
             [5, 10, 14, 17, 19, 20]]
 
 
+def _cgc_dw(x, gs, gr, db_on: bool):
+    """weight / bias gradients of the node blocks: dW_s = gs^T x, dW_r = gr^T x, db = sum(gr)"""
+    return dense.linear_bwd_w(x, gs), dense.linear_bwd_w(x, gr), (ops.sum_rows(gr) if db_on else None)
+
+
+def _cgc_dx(gs, gr, w, d):
+    """gs W_s + gr W_r: two launches of the linear kernel, the second adding the first in its
+    epilogue"""
+    dx = dense.linear_bwd_x(gs, w, 2 * d, d, w_off=0, ld=3 * d)
+    return dense.linear_bwd_x(gr, w, 2 * d, d, w_off=d, ld=3 * d, res=dx)
+
+
 class _CGCConv(torch.autograd.Function):
+    """One edge convolution with the edge features given ([E, D], CSR order): the generic
+    ``CGCLayer.forward`` API.  Every projection runs on the in-tree linear kernels."""
+
     @staticmethod
     def forward(ctx, x, edge_ft, wv, bv, wm, bm, csr: ops.EdgeCSR, row_scale: Optional[torch.Tensor]):
-        x, edge_ft = ops._f32(x), ops._f32(edge_ft)
+        x, edge_ft = ops._f32(x).contiguous(), ops._f32(edge_ft).contiguous()
         n, d = x.shape
         if edge_ft.shape != (csr.num_edges, d) or n != csr.num_nodes:
             raise ValueError(f"CGC shapes: x {tuple(x.shape)}, edge_ft {tuple(edge_ft.shape)}, "
                              f"csr {csr.num_nodes} nodes / {csr.num_edges} edges")
-        w = torch.cat([wv, wm])                                   # [2D, 3D]
-        ws, wr, we = w[:, :d], w[:, d: 2 * d], w[:, 2 * d:]
-        ps = x @ ws.t()
-        pr = torch.addmm(torch.cat([bv, bm]), x, wr.t())
-        ep = edge_ft @ we.t()
+        w = torch.cat([wv, wm]).contiguous()                      # [2D, 3D]
+        b = torch.cat([bv, bm]).contiguous()
+        ps = dense.linear_fwd(x, w, 2 * d, d, w_off=0, ld=3 * d)
+        pr = dense.linear_fwd(x, w, 2 * d, d, w_off=d, ld=3 * d, bias=b)
+        ep = dense.linear_fwd(edge_ft, w, 2 * d, d, w_off=2 * d, ld=3 * d)
         agg = torch.empty(n, d, device=x.device, dtype=torch.float32)
         tok = ops.TIMER.start("cgc_fwd")
         _lib.check(_lib.load().eelg_cgc_fwd(
@@ -57,7 +74,7 @@ class _CGCConv(torch.autograd.Function):
         x, edge_ft, ps, pr, ep, w, row_scale = ctx.saved_tensors
         csr = ctx.csr
         n, d = x.shape
-        g = ops._f32(g)
+        g = ops._f32(g).contiguous()
         dz = torch.empty(csr.num_edges, 2 * d, device=x.device, dtype=torch.float32)
         gr = torch.empty(n, 2 * d, device=x.device, dtype=torch.float32)
         tok = ops.TIMER.start("cgc_bwd")
@@ -66,12 +83,74 @@ class _CGCConv(torch.autograd.Function):
             _lib.ptr(row_scale), n, d, _lib.ptr(g), _lib.ptr(dz), _lib.ptr(gr), _lib.stream(g)), "cgc_bwd")
         ops.TIMER.stop(tok)
         gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)   # per-sender sums of dz
-        ws, wr, we = w[:, :d], w[:, d: 2 * d], w[:, 2 * d:]
-        dw = torch.cat([ops._wgrad(gs, x), ops._wgrad(gr, x), ops._wgrad(dz, edge_ft)], dim=1)
-        db = ops.sum_rows(gr)
-        dx = gs @ ws + gr @ wr
-        dedge = dz @ we
+        dws, dwr, db = _cgc_dw(x, gs, gr, True)
+        dwe = dense.linear_bwd_w(edge_ft, dz)
+        dw = torch.cat([dws, dwr, dwe], dim=1)
+        dx = _cgc_dx(gs, gr, w, d)
+        dedge = dense.linear_bwd_x(dz, w, 2 * d, d, w_off=2 * d, ld=3 * d)
         return dx, dedge, dw[:d], db[:d], dw[d:], db[d:], None, None
+
+
+class _CGCConvEF(torch.autograd.Function):
+    """The model path: edge features in factored form (``eelg_cgc_fwd_ef``), ``ef`` [E, 8] =
+    [e5 | 1 | 0 | 0] (data) and ``ea`` [8, 2D] = [W5^T W_e^T ; b5 W_e^T ; 0] (a differentiable
+    function of the edge embedding and the layer's edge block, formed by ``_edge_factor``).  Its
+    gradient is ef^T dz, read off the same dz the node blocks use."""
+
+    @staticmethod
+    def forward(ctx, x, ea, wv, bv, wm, bm, ef, csr: ops.EdgeCSR, row_scale: Optional[torch.Tensor]):
+        x = ops._f32(x).contiguous()
+        ea = ops._f32(ea).contiguous()
+        n, d = x.shape
+        if ef.shape != (csr.num_edges, 8) or ea.shape != (8, 2 * d) or n != csr.num_nodes:
+            raise ValueError(f"CGC (factored edges) shapes: x {tuple(x.shape)}, ef {tuple(ef.shape)}, "
+                             f"ea {tuple(ea.shape)}, csr {csr.num_nodes} nodes / {csr.num_edges} edges")
+        w = torch.cat([wv, wm]).contiguous()
+        b = torch.cat([bv, bm]).contiguous()
+        ps = dense.linear_fwd(x, w, 2 * d, d, w_off=0, ld=3 * d)
+        pr = dense.linear_fwd(x, w, 2 * d, d, w_off=d, ld=3 * d, bias=b)
+        agg = torch.empty(n, d, device=x.device, dtype=torch.float32)
+        tok = ops.TIMER.start("cgc_fwd")
+        _lib.check(_lib.load().eelg_cgc_fwd_ef(
+            _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
+            _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(agg), _lib.stream(agg)), "cgc_fwd_ef")
+        ops.TIMER.stop(tok)
+        ctx.save_for_backward(x, ea, ef, ps, pr, w, row_scale)
+        ctx.csr = csr
+        return agg
+
+    @staticmethod
+    def backward(ctx, g):
+        x, ea, ef, ps, pr, w, row_scale = ctx.saved_tensors
+        csr = ctx.csr
+        n, d = x.shape
+        g = ops._f32(g).contiguous()
+        dz = torch.empty(csr.num_edges, 2 * d, device=x.device, dtype=torch.float32)
+        gr = torch.empty(n, 2 * d, device=x.device, dtype=torch.float32)
+        tok = ops.TIMER.start("cgc_bwd")
+        _lib.check(_lib.load().eelg_cgc_bwd_ef(
+            _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
+            _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(g), _lib.ptr(dz), _lib.ptr(gr),
+            _lib.stream(g)), "cgc_bwd_ef")
+        ops.TIMER.stop(tok)
+        gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)
+        dws, dwr, db = _cgc_dw(x, gs, gr, True)
+        dea = dense.linear_bwd_w(ef, dz).t()                      # [8, 2D] = ef^T dz
+        zero = torch.zeros(2 * d, d, device=x.device, dtype=torch.float32)
+        dw = torch.cat([dws, dwr, zero], dim=1)                   # the edge block: through ea
+        dx = _cgc_dx(gs, gr, w, d)
+        return dx, dea, dw[:d], db[:d], dw[d:], db[d:], None, None, None
+
+
+def _edge_factor(edge_emb: torch.nn.Linear, we: torch.Tensor) -> torch.Tensor:
+    """ea [8, 2D] with [e5 | 1 | 0 | 0] @ ea = (e5 W5^T + b5) W_e^T: rows 0..4 = W5^T W_e^T, row 5
+    = b5 W_e^T, rows 6..7 zero.  Broadcast products and sums (no GEMM); autograd carries the
+    gradient to the edge embedding and to the layer's edge block."""
+    w5, b5 = edge_emb.weight, edge_emb.bias                       # [D, 5], [D]
+    a = (w5.t()[:, None, :] * we[None, :, :]).sum(-1)           # [5, 2D]
+    c = (we * b5[None, :]).sum(-1)                               # [2D]
+    pad = torch.zeros(2, we.shape[0], device=we.device, dtype=we.dtype)
+    return torch.cat([a, c[None], pad], dim=0)
 
 
 class CGCLayer(torch.nn.Module):
@@ -94,22 +173,38 @@ class CGCLayer(torch.nn.Module):
         self.fc_multip = torch.nn.Linear(self.num_hid_dim, node_dim)
         self.reduction = reduction
 
+    def _scale(self, csr: ops.EdgeCSR) -> Optional[torch.Tensor]:
+        if self.reduction != "mean":
+            return None
+        deg = (csr.rowptr[1:] - csr.rowptr[:-1]).to(torch.float32)
+        return 1.0 / deg.clamp_min(1.0)
+
     def forward(self, x: torch.Tensor, edge_index: EdgeIndex, edge_ft: torch.Tensor) -> torch.Tensor:
         ops._require_device(x)
         csr, edge_ft = as_csr(edge_index, x.shape[0], edge_ft)
-        scale = None
-        if self.reduction == "mean":
-            deg = (csr.rowptr[1:] - csr.rowptr[:-1]).to(torch.float32)
-            scale = 1.0 / deg.clamp_min(1.0)
         return _CGCConv.apply(x, edge_ft, self.fc_values.weight, self.fc_values.bias,
-                              self.fc_multip.weight, self.fc_multip.bias, csr, scale)
+                              self.fc_multip.weight, self.fc_multip.bias, csr, self._scale(csr))
+
+    def edge_block(self) -> torch.Tensor:
+        """W_e [2D, D]: the edge-feature columns of [W_values; W_multip]"""
+        d = self.fc_values.out_features
+        return torch.cat([self.fc_values.weight[:, 2 * d:], self.fc_multip.weight[:, 2 * d:]])
+
+    def forward_factored(self, x: torch.Tensor, csr: ops.EdgeCSR, ef: torch.Tensor,
+                         ea: torch.Tensor) -> torch.Tensor:
+        """The same layer on factored edge features (``_CGCConvEF``): ``ef`` [E, 8] =
+        [e5 | 1 | 0 | 0] in CSR order, ``ea`` = ``_edge_factor(edge embedding, edge_block())``."""
+        ops._require_device(x)
+        return _CGCConvEF.apply(x, ea, self.fc_values.weight, self.fc_values.bias,
+                                self.fc_multip.weight, self.fc_multip.bias, ef, csr,
+                                self._scale(csr))
 
 
 def _head(hidden: int) -> torch.nn.Sequential:
-    return torch.nn.Sequential(torch.nn.Linear(hidden, 128), torch.nn.Softplus(),
-                               torch.nn.Linear(128, 64), torch.nn.Softplus(),
-                               torch.nn.Linear(64, 32), torch.nn.Softplus(),
-                               torch.nn.Linear(32, 21))
+    return torch.nn.Sequential(dense.Linear(hidden, 128), torch.nn.Softplus(),
+                               dense.Linear(128, 64), torch.nn.Softplus(),
+                               dense.Linear(64, 32), torch.nn.Softplus(),
+                               dense.Linear(32, 21))
 
 
 def _edge_inputs(batch, csr: ops.EdgeCSR) -> torch.Tensor:
@@ -128,7 +223,9 @@ class _CGCBase(torch.nn.Module):
         super().__init__()
         self.params = params
         hid = params.hidden_irreps
-        self.node_ft_embedding = torch.nn.Linear(self.node_inputs, hid)
+        # K = 1 / 3 inputs: broadcast multiply-adds; the edge embedding's parameters enter each
+        # layer through _edge_factor (the [E, hid] edge features are never formed)
+        self.node_ft_embedding = dense.SmallInLinear(self.node_inputs, hid)
         self.edge_ft_embedding = torch.nn.Linear(5, hid)
         self.cgc_layers = torch.nn.ModuleList(
             [CGCLayer(hid, hid, params.interaction_reduction) for _ in range(params.message_passes)])
@@ -136,9 +233,16 @@ class _CGCBase(torch.nn.Module):
         self.mlp = _head(hid)
 
     def _encode(self, batch, node_in):
+        """(csr, node embedding, ef [E, 8] = [e5 | 1 | 0 | 0] in CSR order)"""
         from .model import EnergyEquivGNN
         csr = EnergyEquivGNN.edge_graph(batch)
-        return csr, self.node_ft_embedding(node_in), self.edge_ft_embedding(_edge_inputs(batch, csr))
+        e5 = _edge_inputs(batch, csr)
+        ef = torch.cat([e5, torch.ones_like(e5[:, :1]), torch.zeros_like(e5[:, :2])], dim=1).contiguous()
+        return csr, self.node_ft_embedding(node_in), ef
+
+    def _layer(self, i, h, csr, ef):
+        layer = self.cgc_layers[i]
+        return layer.forward_factored(h, csr, ef, _edge_factor(self.edge_ft_embedding, layer.edge_block()))
 
     def _pool(self, h, batch):
         return ops.graph_pool(h, batch.batch, batch.num_graphs, self.global_reduction)
@@ -152,9 +256,9 @@ class CrystGraphConv(_CGCBase):
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         csr, h, ef = self._encode(batch, batch.node_attrs)
-        h = self.cgc_layers[0](h, csr, ef)
-        for layer in self.cgc_layers[1:]:
-            h = h + layer(h, csr, ef)
+        h = self._layer(0, h, csr, ef)
+        for i in range(1, len(self.cgc_layers)):
+            h = h + self._layer(i, h, csr, ef)
         a = self.mlp(self._pool(h, batch))[:, self.inds_val]
         if self.params.positive == "square":
             return {"stiffness": torch.linalg.matrix_power(a, 2)}
@@ -170,6 +274,6 @@ class CrystGraphConvVanilla(_CGCBase):
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         csr, h, ef = self._encode(batch, batch.positions)
-        for layer in self.cgc_layers:
-            h = h + layer(h, csr, ef)
+        for i in range(len(self.cgc_layers)):
+            h = h + self._layer(i, h, csr, ef)
         return {"stiffness": self.mlp(self._pool(h, batch))}

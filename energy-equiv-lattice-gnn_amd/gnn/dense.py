@@ -1,0 +1,141 @@
+"""Dense ``torch.nn.Linear`` layers on the in-tree fp32 MFMA linear kernels (``eelg_linear_*``).
+
+The CGC / mCGC benchmark models (``scripts/benchmark_models/cgc_modified.py:11-88``,
+``cgc_vanilla.py:11-74``) are chains of plain Linear layers around the edge convolution.  A
+Linear ``y = x W^T + b`` is the channel-mixing linear of ``o3.Linear`` with one scalar slot
+(``d = 1``), so the same kernels run it: the descriptor reads ``W`` in torch layout
+(``B[k][j] = W[j, k]``: ``ldk = 1``, ``ldj = ld``), the gradient w.r.t. ``x`` swaps the strides
+(``gx = gy W``), and the weight gradient comes from ``eelg_linear_bwd_w`` as per-node-slice
+partials summed in a fixed order (``ops.sum_rows``), so no library GEMM runs.  ``w_off`` / ``ld``
+address a column block of a wider weight (the sender / receiver / edge blocks of the CGC layer's
+``[2D, 3D]`` weight) without a copy.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib, ops
+
+LINW_WG = 4096          # weight-gradient workgroups (node slices x 32x32 tiles), as o3.Linear
+LINW_MAX_SLICES = 128
+
+
+def _slot_desc(n_out: int, k: int, w_off: int, ldk: int, ldj: int, bias: bool, n: int):
+    d = _lib.LinDesc()
+    d.n_slots = 1
+    d.max_jt = (n_out + 31) // 32
+    d.max_rows = n
+    sl = d.slot[0]
+    sl.y_off, sl.n_out, sl.d = 0, n_out, 1
+    sl.bias_off = 0 if bias else -1
+    sl.n_src = 1
+    s = sl.src[0]
+    s.x_off, s.k, s.w_off, s.ldk, s.ldj, s.alpha = 0, k, w_off, ldk, ldj, 1.0
+    return d
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, n_out: int, k: int, w_off: int = 0,
+               ld: Optional[int] = None, bias: Optional[torch.Tensor] = None,
+               res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x[:, :k] @ W_blk^T (+ bias) (+ res)`` with ``W_blk[j, c] = w.flat[w_off + j * ld + c]``
+    (a column block of a row-major ``[n_out, ld]`` weight)."""
+    ld = k if ld is None else ld
+    n = x.shape[0]
+    y = torch.empty(n, n_out, device=x.device, dtype=torch.float32)
+    desc = _slot_desc(n_out, k, w_off, 1, ld, bias is not None, n)
+    _lib.check(_lib.load().eelg_linear_fwd_res(
+        _lib.ptr(x), x.shape[1], _lib.ptr(w), _lib.ptr(bias), _lib.ptr(res), n, _lib.ptr(y), n_out,
+        ctypes.byref(desc), _lib.stream(y)), "dense_fwd")
+    return y
+
+
+def linear_bwd_x(gy: torch.Tensor, w: torch.Tensor, n_out: int, k: int, w_off: int = 0,
+                 ld: Optional[int] = None, res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``gy @ W_blk (+ res)``: the gradient of ``linear_fwd`` w.r.t. ``x`` ([N, k])."""
+    ld = k if ld is None else ld
+    n = gy.shape[0]
+    gx = torch.empty(n, k, device=gy.device, dtype=torch.float32)
+    desc = _slot_desc(k, n_out, w_off, ld, 1, False, n)
+    _lib.check(_lib.load().eelg_linear_fwd_res(
+        _lib.ptr(gy), gy.shape[1], _lib.ptr(w), None, _lib.ptr(res), n, _lib.ptr(gx), k,
+        ctypes.byref(desc), _lib.stream(gx)), "dense_bwd_x")
+    return gx
+
+
+def linear_bwd_w(x: torch.Tensor, gy: torch.Tensor) -> torch.Tensor:
+    """``gy^T @ x`` ([n_out, k], torch weight layout) over the rows of ``x`` [N, k] / ``gy``
+    [N, n_out]: node-slice partials of ``x^T gy`` (``eelg_linear_bwd_w``) summed in a fixed order,
+    then transposed."""
+    n, k = x.shape
+    n_out = gy.shape[1]
+    if n == 0:
+        return torch.zeros(n_out, k, device=x.device, dtype=torch.float32)
+    tiles = ((k + 31) // 32) * ((n_out + 31) // 32)
+    slices = max(1, min((n + 31) // 32, -(-LINW_WG // tiles), LINW_MAX_SLICES))
+    nps = -(-n // slices)
+    slices = -(-n // nps)
+    wd = _lib.LinWDesc()
+    wd.n_ins, wd.max_jt, wd.max_ut, wd.max_rows = 1, (n_out + 31) // 32, (k + 31) // 32, n
+    e = wd.ins[0]
+    e.x_off, e.k, e.g_off, e.n_out, e.d, e.w_off, e.alpha = 0, k, 0, n_out, 1, 0, 1.0
+    part = torch.empty(slices, k * n_out, device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().eelg_linear_bwd_w(
+        _lib.ptr(x), k, _lib.ptr(gy), n_out, n, nps, _lib.ptr(part), slices, k * n_out,
+        ctypes.byref(wd), _lib.stream(part)), "dense_bwd_w")
+    return ops.sum_rows(part).view(k, n_out).t()
+
+
+class _DenseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = ops._f32(x).contiguous()
+        n_out, k = weight.shape
+        y = linear_fwd(x, weight.contiguous(), n_out, k, bias=bias)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = ops._f32(gy).contiguous()
+        n_out, k = weight.shape
+        gx = linear_bwd_x(gy, weight.contiguous(), n_out, k) if ctx.needs_input_grad[0] else None
+        gw = linear_bwd_w(x, gy) if ctx.needs_input_grad[1] else None
+        gb = ops.sum_rows(gy) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+class Linear(torch.nn.Linear):
+    """``torch.nn.Linear`` (same parameters, initialisation and state_dict) whose forward and
+    backward run on the HIP linear kernels; device tensors only (no CPU fallback)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        ops._require_device(x)
+        shape = x.shape
+        y = _DenseFn.apply(x.reshape(-1, shape[-1]), self.weight, self.bias)
+        return y.view(*shape[:-1], self.out_features)
+
+
+def small_in_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """``x @ W^T + b`` for a handful of inputs (the node embeddings, K = 1 or 3) as broadcast
+    multiply-adds: a K-term outer product is elementwise work, not a GEMM."""
+    out = bias.expand(x.shape[0], -1) if bias is not None else None
+    for c in range(x.shape[1]):
+        term = x[:, c: c + 1] * weight[:, c]
+        out = term if out is None else out + term
+    return out
+
+
+class SmallInLinear(torch.nn.Linear):
+    """``torch.nn.Linear`` with few inputs (K <= 8) evaluated by ``small_in_linear``."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return small_in_linear(x, self.weight, self.bias)
+
+
+__all__ = ["Linear", "SmallInLinear", "linear_fwd", "linear_bwd_x", "linear_bwd_w",
+           "small_in_linear"]

@@ -142,3 +142,63 @@ def test_cgc_model_fullsize_matches_oracle(variant):
     assert _rel(cm, co) < 1e-4
     for k, q in m.named_parameters():
         assert _rel(q.grad, po[k].grad) < 2e-5, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n_out,bias", [(128, 256, True), (96, 192, False), (64, 21, True),
+                                          (32, 64, True), (5, 128, True)])
+def test_dense_linear_matches_torch(k, n_out, bias):
+    """``gnn.dense.Linear`` (the CGC models' Linear layers on the in-tree MFMA kernels): output,
+    grad-x, grad-W and grad-b against the fp64 torch Linear, 2e-6 of the largest entry (fp32
+    sums over K / over the rows)."""
+    from gnn import dense
+    torch.manual_seed(3)
+    ref = torch.nn.Linear(k, n_out, bias=bias).double()
+    m = dense.Linear(k, n_out, bias=bias).cuda()
+    m.load_state_dict({kk: v.float() for kk, v in ref.state_dict().items()})
+    x = torch.randn(1000, k, dtype=F64)
+    xo, xm = x.clone().requires_grad_(True), x.float().cuda().requires_grad_(True)
+    yo, ym = ref(xo), m(xm)
+    g = torch.randn_like(yo)
+    (yo * g).sum().backward()
+    (ym * g.float().cuda()).sum().backward()
+    assert _rel(ym, yo) < 2e-6
+    assert _rel(xm.grad, xo.grad) < 2e-6
+    assert _rel(m.weight.grad, ref.weight.grad) < 2e-6
+    if bias:
+        assert _rel(m.bias.grad, ref.bias.grad) < 2e-6
+
+
+@pytest.mark.gpu
+def test_cgc_factored_edges_match_generic_layer():
+    """``CGCLayer.forward_factored`` (edge features as [e5 | 1] @ A, eelg_cgc_fwd_ef) equals the
+    generic ``forward`` on the materialised edge features e5 W5^T + b5 (two fp32 evaluations in
+    different association orders: 1e-5 of the largest entry), gradients w.r.t. x and the layer
+    weights included, and the edge embedding's gradients agree."""
+    from gnn import cgc
+    from gnn.model import EnergyEquivGNN
+    torch.manual_seed(4)
+    d = 128
+    layer = cgc.CGCLayer(d, d).cuda()
+    emb = torch.nn.Linear(5, d).cuda()
+    b, _ = batch(3, 40, 160, 17)
+    bd = b.to("cuda")
+    csr = EnergyEquivGNN.edge_graph(bd)
+    e5 = cgc._edge_inputs(bd, csr)
+    ef = torch.cat([e5, torch.ones_like(e5[:, :1]), torch.zeros_like(e5[:, :2])], 1).contiguous()
+    x = torch.randn(csr.num_nodes, d, device="cuda")
+    g = torch.randn(csr.num_nodes, d, device="cuda")
+
+    def run(factored):
+        for p in list(layer.parameters()) + list(emb.parameters()):
+            p.grad = None
+        xr = x.clone().requires_grad_(True)
+        if factored:
+            y = layer.forward_factored(xr, csr, ef, cgc._edge_factor(emb, layer.edge_block()))
+        else:
+            y = layer(xr, csr, emb(e5))
+        (y * g).sum().backward()
+        return [y.detach(), xr.grad] + [p.grad.clone() for p in list(layer.parameters()) + list(emb.parameters())]
+    a, r = run(True), run(False)
+    for u, v in zip(a, r):
+        assert _rel(u, v) < 1e-5

@@ -549,7 +549,7 @@ def test_model_global_reduction_mul_is_not_degenerate():
     readout features (|x| ~ 1e-2) underflows to ~0, so the stiffness is then a constant and the
     comparison checks nothing.  Here the graphs have 4 nodes and the readout's last linear is
     scaled 30x, so the pooled products are O(1e-3 .. 1e4) (asserted) and every node's features
-    reach the output; stiffness / loss 1e-4, every parameter gradient 1e-5 of its max."""
+    reach the output; stiffness / loss 1e-4; parameter gradients: see below."""
     import oracle.model as om
     from gnn.model import EnergyEquivGNN
     from gnn.train import stiffness_loss
@@ -581,14 +581,28 @@ def test_model_global_reduction_mul_is_not_degenerate():
     lm = stiffness_loss(cm, bd.stiffness)
     lm.backward()
     g = cap["pooled"].abs()
+    # the product pool is ill-conditioned (|pooled| spans 1e-3 .. 1e4): torch's own fp32 run of
+    # the same oracle carries the gradient error that any fp32 arithmetic carries here, so the
+    # device's parameter gradients must be within 2x of that error (and within 1e-5 where it is
+    # smaller)
+    of = omodel.EnergyEquivGNN(p).float()
+    of.load_state_dict(o.state_dict())
+    bf = batch_to(b, "cpu", torch.float32)
+    oracle_loss(of(bf)["stiffness"], bf.stiffness).backward()
     po = dict(o.named_parameters())
-    worst = max(rel_err(pm.grad, po[name].grad) for name, pm in m.named_parameters())
+    pf = dict(of.named_parameters())
+    worst, worst_f32, ratio = 0.0, 0.0, 0.0
+    for name, pm in m.named_parameters():
+        e, ef = rel_err(pm.grad, po[name].grad), rel_err(pf[name].grad, po[name].grad)
+        worst, worst_f32 = max(worst, e), max(worst_f32, ef)
+        assert e < max(1e-5, 2.0 * ef), (name, e, ef)
+        ratio = max(ratio, e / max(ef, 1e-12))
     record_parity("model_reduce_mul", stiffness=rel_err(cm, co), grad_params=worst,
+                  grad_params_torch_fp32=worst_f32, worst_ratio_to_fp32=ratio,
                   pooled_median=float(g.median()), pooled_max=float(g.max()))
     assert float(g.median()) > 1e-4 and float(g.max()) > 1.0, (float(g.median()), float(g.max()))
     assert rel_err(cm, co) < 1e-4
     assert abs(lm.item() - lo.item()) <= 1e-4 * abs(lo.item())
-    assert worst < 1e-5
 
 
 @pytest.mark.parametrize("irreps_in,irreps_out", [

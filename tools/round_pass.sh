@@ -5,7 +5,7 @@
 #
 # usage (GPU box): bash tools/round_pass.sh <tag> <step> [<step> ...]
 #   tests                 the whole `pytest -m gpu` suite (EELG_PARITY_OUT -> parity.json)
-#   pytest:<args>         pytest -m gpu over <args> (files, `-k expr` with spaces as '+')
+#   pytest:<files>[:<k>]  pytest -m gpu over <files> ('+' between files), -k <k> ('+' for spaces)
 #   smoke                 __graft_entry__.smoke()
 #   bench[:<args>]        bench.py line (args with '+' for spaces, e.g. bench:--config+5)
 #   prof:<name>[:<args>]  tools/profile_round.sh for a workload (bench args as above)
@@ -31,8 +31,10 @@ for s in "$@"; do
   case "$s" in
     tests)     step tests.log 900 env EELG_PARITY_OUT="$O/parity.json" $PYT tests -m gpu
                grep -E "FAILED|passed|failed" "$O/tests.log" | tail -5 ;;
-    pytest:*)  a=$(sp "${s#pytest:}"); n=$(echo "${s#pytest:}" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)
-               eval "step t_$n.log 600 env EELG_PARITY_OUT=$O/parity_$n.json $PYT -m gpu $a" ;;
+    pytest:*)  r=${s#pytest:}; f=$(sp "${r%%:*}"); k=""; [ "$r" != "${r%%:*}" ] && k=$(sp "${r#*:}")
+               n=$(echo "$r" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)
+               if [ -n "$k" ]; then step "t_$n.log" 600 env EELG_PARITY_OUT="$O/parity_$n.json" $PYT -m gpu $f -k "$k"
+               else step "t_$n.log" 600 env EELG_PARITY_OUT="$O/parity_$n.json" $PYT -m gpu $f; fi ;;
     smoke)     step smoke.log 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)     step bench.json 400 python3 bench.py ;;
     bench:*)   a=$(sp "${s#bench:}"); n=$(echo "${s#bench:}" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40)
