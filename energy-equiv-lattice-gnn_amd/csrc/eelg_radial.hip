@@ -528,8 +528,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RAD_SMALL_W
 // transpose.  The 4 waves' accumulators are summed through LDS once, at the end.
 // waves per SIMD: 2 (256 registers) where the accumulators fit, else 1 (hidden 64 with 2 hidden
 // layers: 96 accumulator registers + the tile's; EELG build flag RAD_S2_H64N2 picks the kernel)
+#ifndef RAD_S2_WPE64
+#define RAD_S2_WPE64 1   // waves per SIMD asked for hidden 64 with >= 2 hidden layers
+#endif
 template <int H, int NH>
-constexpr int rad_s2_wpe() { return (H == 64 && NH >= 2) ? 1 : 2; }
+constexpr int rad_s2_wpe() { return (H == 64 && NH >= 2) ? RAD_S2_WPE64 : 2; }
 template <int H, int NH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rad_s2_wpe<H, NH>()))) void radial_bwd_small2_kernel(
     const float* __restrict__ ghin, int n_edges, eelg_radial_desc d, const float* __restrict__ zsave,
@@ -689,6 +692,96 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rad_s2_wpe<
       dst[off + threadIdx.x] = s;
     }
     off += H;
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// backward 2, chain form (round 5): only the chain through SiLU' and the hidden layers, no
+// weight gradients.  A wave owns one 32-edge tile (grid-stride), in the MFMA C layout; for
+// n = NH-1 .. 0 it turns grad_h into gz_n = grad_h * SiLU'(z_n) and stores it, stores the layer
+// input h_n = SiLU(z_{n-1}) (n > 0; z_{n-1} is kept for the next layer's SiLU'), and forms the
+// grad_h of the layer below, gz_n W_n, through a wave-private LDS transpose.  The weight and bias
+// gradients (gz_n^T h_n, gz_0^T feats, column sums of gz_n) are then long-K reductions that the
+// linear weight-gradient kernel and eelg_sum_rows run (gnn/ops.py): the fused form kept 96
+// accumulator registers per wave across its tiles and ran at one to two waves per SIMD with
+// scratch spills (0.24 ms at the bench shape, 11.5 % MFMA busy, profiles/r04l_pmc.md).
+template <int H, int NH>
+__global__ __launch_bounds__(256) void radial_bwd_chain_kernel(
+    const float* __restrict__ ghin, int n_edges, eelg_radial_desc d, const float* __restrict__ zsave,
+    float* __restrict__ gz, float* __restrict__ hin) {
+  constexpr int HS = H + 1, NT = H / 32, KH = H / 2, NHM = NH > 1 ? NH - 1 : 1;
+  __shared__ float G[4 * 32 * HS];
+  __shared__ float WS[NHM * H * H];   // W_1 .. W_{NH-1} (the chain's B operand)
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
+  const int ntile = (n_edges + 31) >> 5;
+  float* __restrict__ gw_ = G + wave * 32 * HS;
+  const uint32_t E32 = (uint32_t)n_edges;
+  const rad_rsrc_t rgh = rad_rsrc(ghin, E32 * H * 4u);
+  const rad_rsrc_t rzs = rad_rsrc(zsave, (uint32_t)NH * E32 * H * 4u);
+  const rad_rsrc_t rgz = rad_rsrc(gz, (uint32_t)NH * E32 * H * 4u);
+  const rad_rsrc_t rhi = rad_rsrc(hin, (uint32_t)NHM * E32 * H * 4u);
+#pragma unroll
+  for (int n = 1; n < NH; ++n)
+    for (int e = threadIdx.x; e < H * H; e += 256) WS[(n - 1) * H * H + e] = d.w[n][e];
+  __syncthreads();
+  for (int t = blockIdx.x * 4 + wave; t < ntile; t += gridDim.x * 4) {
+    const int e0 = t * 32;
+    rad_f32x16 gh[NT], zc[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = e0 + rad_row(r, hf);
+        const uint32_t o = ((uint32_t)row * H + ct * 32 + i) * 4u;
+        gh[ct][r] = rad_bld(rgh, rad_off(o, row < n_edges));
+        zc[ct][r] = rad_bld(rzs, rad_off((uint32_t)(NH - 1) * E32 * H * 4u + o, row < n_edges));
+      }
+#pragma unroll
+    for (int n = NH - 1; n >= 0; --n) {
+      __builtin_amdgcn_sched_barrier(0);
+      // gz_n = grad_h * SiLU'(z_n), stored (rows past E dropped by the buffer range check)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = e0 + rad_row(r, hf);
+          gh[ct][r] = rad_silu_grad(zc[ct][r], gh[ct][r]);
+          rad_bst(rgz, rad_off((((uint32_t)n * E32 + row) * H + ct * 32 + i) * 4u, row < n_edges), gh[ct][r]);
+        }
+      if (n > 0) {
+        // the layer input h_n = SiLU(z_{n-1}); z_{n-1} stays for the next layer's SiLU'
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = e0 + rad_row(r, hf);
+            const uint32_t o = ((uint32_t)row * H + ct * 32 + i) * 4u;
+            zc[ct][r] = rad_bld(rzs, rad_off((uint32_t)(n - 1) * E32 * H * 4u + o, row < n_edges));
+            rad_bst(rhi, rad_off((uint32_t)(n - 1) * E32 * H * 4u + o, row < n_edges), rad_silu(zc[ct][r]));
+          }
+        // grad_h of the layer below: gh[e][c] = sum_j gz[e][j] W_n[j][c] (the wave's rows on the
+        // lanes through its LDS transpose)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gw_[rad_row(r, hf) * HS + ct * 32 + i] = gh[ct][r];
+        __builtin_amdgcn_wave_barrier();
+        float a3[KH];
+#pragma unroll
+        for (int st = 0; st < KH; ++st) a3[st] = gw_[i * HS + hf * KH + st];
+        __builtin_amdgcn_wave_barrier();
+        const float* __restrict__ wn = WS + (n - 1) * H * H;
+#pragma unroll
+        for (int c2 = 0; c2 < NT; ++c2) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gh[c2][r] = 0.0f;
+#pragma unroll
+          for (int st = 0; st < KH; ++st)
+            gh[c2] = RAD_MFMA(a3[st], wn[(hf * KH + st) * H + c2 * 32 + i], gh[c2]);
+        }
+      }
+    }
   }
 }
 
@@ -906,6 +999,38 @@ int eelg_radial_fwd(const float* feats, int n_edges, const eelg_radial_desc* d, 
   const unsigned short* wop = static_cast<const unsigned short*>(wo_parts);
   RAD_LAUNCH3(radial_fwd_kernel, grid, feats, n_edges, *d, wop, zsave, out);
   return eelg_check_launch("radial_fwd");
+}
+
+int eelg_radial_bwd_chain(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
+                          const void* wot_parts, const float* zsave, float* grad_h, float* gz,
+                          float* hin, float* part_wo, void* stream) {
+  if (int rc = radial_check(d, n_edges, grad_bf16 ? 2 : 4)) return rc;
+  if (!rad_a16(wot_parts) || !rad_a16(grad_w))
+    return eelg_fail(-2, "radial_bwd_chain: grad_w and wot_parts must be 16-byte aligned");
+  if (d->hidden != 64) return eelg_fail(-2, "radial_bwd_chain: hidden %d not built (64)", d->hidden);
+  if (n_edges == 0) return 0;
+  const unsigned short* wotp = static_cast<const unsigned short*>(wot_parts);
+  hipStream_t st = (hipStream_t)stream;
+  const bool bf = grad_bf16 != 0;
+  int nw, ns, tps;
+  radial_plan(n_edges, d->n_out, &nw, &ns, &tps);
+  const dim3 g1((n_edges + 127) / 128);
+  const int W = d->n_out;
+  if (bf) hipLaunchKernelGGL((radial_bwd_gh_kernel<64, true>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
+  else hipLaunchKernelGGL((radial_bwd_gh_kernel<64, false>), g1, dim3(256), 0, st, grad_w, n_edges, W, wotp, grad_h);
+  if (int rc = eelg_check_launch("radial_bwd_gh")) return rc;
+  const int ntile = (n_edges + 31) / 32;
+  const dim3 g2((unsigned)((ntile + 3) / 4 < 2048 ? (ntile + 3) / 4 : 2048));
+  if (d->n_hidden == 1)
+    hipLaunchKernelGGL((radial_bwd_chain_kernel<64, 1>), g2, dim3(256), 0, st, grad_h, n_edges, *d, zsave, gz, hin);
+  else if (d->n_hidden == 2)
+    hipLaunchKernelGGL((radial_bwd_chain_kernel<64, 2>), g2, dim3(256), 0, st, grad_h, n_edges, *d, zsave, gz, hin);
+  else
+    hipLaunchKernelGGL((radial_bwd_chain_kernel<64, 3>), g2, dim3(256), 0, st, grad_h, n_edges, *d, zsave, gz, hin);
+  if (int rc = eelg_check_launch("radial_bwd_chain")) return rc;
+  const dim3 g3((W + 127) / 128, ns);
+  RAD_LAUNCH3(radial_bwd_wo_kernel, g3, grad_w, n_edges, W, zsave, tps, part_wo);
+  return eelg_check_launch("radial_bwd_wo");
 }
 
 int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,

@@ -65,6 +65,7 @@ _SIGS = {
     "eelg_sum_rows": ([_P, ctypes.c_longlong, _I, ctypes.c_longlong, ctypes.c_float, _P, _P,
                        ctypes.c_longlong, _P], _I),
     "eelg_radial_fwd": ([_P, _I, _P, _P, _I, _P, _P, _P], _I),
+    "eelg_radial_bwd_chain": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
     "eelg_radial_bwd": ([_P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], _I),
 }
 

@@ -56,6 +56,9 @@ OVERLAP = os.environ.get("EELG_OVERLAP", "1") != "0"
 SC_CMAJOR_ON_SIDE = os.environ.get("EELG_SC_CMAJOR_SIDE", "0") != "0"   # measured equal; fused keeps fewer bytes
 # the contraction's coefficient gradient on the coefficient side stream (1) or in line (0)
 SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
+# radial MLP backward (hidden 64): the chain kernel + weight gradients on the linear kernels (1),
+# or the fused small-layer kernel with per-workgroup partials (0)
+RADIAL_CHAIN = os.environ.get("EELG_RADIAL_CHAIN", "1") != "0"
 # TP backward in sender order (eelg_tp_bwd_sender) instead of per-edge gxe + sender segment sum:
 # "1" always, "0" never, "auto" (default) for bf16 storage only.  fp32: measured slower (r02s1:
 # tp_bws 1.40 ms vs tp_bwd 1.05 + sender sum 0.16 ms; 1832 vs 1862 graphs/s) -- each edge
@@ -653,6 +656,8 @@ class _RadialMLP(torch.autograd.Function):
         lib = _lib.load()
         wot_parts = split_bf16x3(wo.t().contiguous())             # [3, hidden, n_out]
         h = d.hidden
+        if RADIAL_CHAIN and h == 64:
+            return _RadialMLP._backward_chain(ctx, g, feats, params, zs, d, wot_parts, wp, n_out)
         n_small = h * nf + h + (d.n_hidden - 1) * (h * h + h)
         small, gwo = None, None
         for (a, b), z in zip(ctx.chunks, zs):
@@ -677,6 +682,43 @@ class _RadialMLP(torch.autograd.Function):
         for p in params[:-1]:
             grads.append(small[off: off + p.numel()].view_as(p))
             off += p.numel()
+        grads.append(gwo if wp == n_out else gwo[:n_out].contiguous())
+        return (None, None, *grads)
+
+    @staticmethod
+    def _backward_chain(ctx, g, feats, params, zs, d, wot_parts, wp, n_out):
+        """``eelg_radial_bwd_chain``: the kernels leave gz_n and the hidden-layer inputs; the
+        weight gradients gz_n^T h_n are long-K reductions on the linear weight-gradient kernel and
+        the bias gradients column sums (``eelg_sum_rows``), all in a fixed order"""
+        from . import dense
+        lib = _lib.load()
+        h, nh = d.hidden, d.n_hidden
+        acc = [None] * (2 * nh)
+        gwo = None
+        for (a, b), z in zip(ctx.chunks, zs):
+            ec = b - a
+            npart, ns = ctypes.c_int(), ctypes.c_int()
+            _lib.check(lib.eelg_radial_plan(ec, d.n_out, ctypes.byref(npart), ctypes.byref(ns)),
+                       "radial_plan")
+            part_wo = torch.empty(ns.value, d.n_out, h, device=g.device, dtype=torch.float32)
+            grad_h = torch.empty(ec, h, device=g.device, dtype=torch.float32)
+            gz = torch.empty(nh, ec, h, device=g.device, dtype=torch.float32)
+            hin = torch.empty(max(nh - 1, 1), ec, h, device=g.device, dtype=torch.float32)
+            if ec == 0:
+                part_wo.zero_()
+            _lib.check(lib.eelg_radial_bwd_chain(_lib.ptr(g[a:b]), int(g.dtype == torch.bfloat16), ec,
+                                                 ctypes.byref(d), _lib.ptr(wot_parts), _lib.ptr(z),
+                                                 _lib.ptr(grad_h), _lib.ptr(gz), _lib.ptr(hin),
+                                                 _lib.ptr(part_wo), _lib.stream(g)), "radial_bwd_chain")
+            for n in range(nh):
+                x_n = feats[a:b] if n == 0 else hin[n - 1]
+                gw = dense.linear_bwd_w(x_n, gz[n]) if ec else torch.zeros_like(params[2 * n])
+                gb = sum_rows(gz[n]) if ec else torch.zeros_like(params[2 * n + 1])
+                acc[2 * n] = gw if acc[2 * n] is None else acc[2 * n] + gw
+                acc[2 * n + 1] = gb if acc[2 * n + 1] is None else acc[2 * n + 1] + gb
+            wo = sum_rows(part_wo)
+            gwo = wo if gwo is None else gwo + wo
+        grads = [t.view_as(p) for t, p in zip(acc, params[:-1])]
         grads.append(gwo if wp == n_out else gwo[:n_out].contiguous())
         return (None, None, *grads)
 

@@ -307,6 +307,14 @@ int eelg_radial_plan(int n_edges, int n_out, int* n_part, int* n_split);
 int eelg_radial_bwd(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
                     const void* wot_parts, const float* zsave, const float* feats, float* grad_h,
                     float* part_h, float* part_wo, void* stream);
+/* The same backward with the hidden-layer weight and bias gradients left to the caller (hidden
+ * 64): grad_h as above; gz[n_hidden, E, 64] = grad of the pre-activations z_n; hin[n_hidden - 1,
+ * E, 64] = the inputs SiLU(z_{n-1}) of the hidden layers n >= 1; part_wo as above.  The caller
+ * forms grad W_n = gz_n^T hin_n (n >= 1), grad W_0 = gz_0^T feats and grad b_n = column sums of
+ * gz_n (eelg_linear_bwd_w / eelg_sum_rows). */
+int eelg_radial_bwd_chain(const void* grad_w, int grad_bf16, int n_edges, const eelg_radial_desc* d,
+                          const void* wot_parts, const float* zsave, float* grad_h, float* gz,
+                          float* hin, float* part_wo, void* stream);
 
 /* Deterministic sum over the leading dimension of partial results (the partial buffers of
  * eelg_linear_bwd_w, eelg_radial_bwd and eelg_sc_bwd_coef, and the bias gradients = column

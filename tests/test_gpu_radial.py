@@ -149,3 +149,32 @@ def test_radial_split_gemm_as_accurate_as_fp32(hidden, n_out):
     print("rel err vs fp64 (device, torch fp32):", errs)   # shown on failure
     for name, (es, ef) in errs.items():
         assert es <= 1.5 * ef + 1e-7, (name, es, ef)
+
+
+@pytest.mark.parametrize("n_edges,layers,bf16", [(4096, 3, False), (1000, 2, False), (77, 4, False),
+                                                 (4096, 3, True)])
+def test_radial_chain_backward_matches_fused_backward(n_edges, layers, bf16, monkeypatch):
+    """hidden 64: the chain backward (``eelg_radial_bwd_chain`` + weight gradients on the linear
+    weight-gradient kernel + column sums) against the fused small-layer kernel
+    (``eelg_radial_bwd``), same inputs: the output-weight gradient bitwise (same kernel), the
+    hidden-layer gradients within 2e-6 of their max (another fp32 summation order)."""
+    from gnn import ops
+    dev = _mlp(12, 64, layers, 1344, seed=5).to(DEV)
+    torch.manual_seed(2)
+    feats = (torch.rand(n_edges, 12) * 0.9).to(DEV)
+    g = torch.randn(n_edges, 1344, device=DEV)
+    dt = torch.bfloat16 if bf16 else torch.float32
+
+    def grads(chain):
+        monkeypatch.setattr(ops, "RADIAL_CHAIN", chain)
+        for p in dev.parameters():
+            p.grad = None
+        y = ops.radial_mlp(feats, dev, out_dtype=dt)
+        y.backward(g.to(dt))
+        return [p.grad.clone() for p in dev.parameters()]
+    a, b = grads(True), grads(False)
+    for k, (u, v) in enumerate(zip(a, b)):
+        if k == len(a) - 1:
+            assert torch.equal(u, v)
+        else:
+            assert rel_err(u, v) < 2e-6, k
