@@ -19,8 +19,24 @@
 // the [8, 2D] A instead of the [E, 2D] Ep (1 KiB per edge at D = 128), and form Ep in registers.
 #include <hip/hip_runtime.h>
 
+#ifndef CGC_FAST_MATH
+#define CGC_FAST_MATH 1
+#endif
+#if CGC_FAST_MATH
+// hardware exp2 / log2 / reciprocal (v_exp_f32, v_log_f32, v_rcp_f32: about 1 ulp each):
+// softplus(z) = max(z, 0) + log(1 + exp(-|z|)) never overflows and keeps torch's threshold
+__device__ __forceinline__ float cgc_softplus(float z) {
+  if (z > 20.0f) return z;
+  const float t = __builtin_amdgcn_exp2f(-fabsf(z) * 1.4426950408889634f);
+  return fmaxf(z, 0.0f) + __builtin_amdgcn_logf(1.0f + t) * 0.6931471805599453f;
+}
+__device__ __forceinline__ float cgc_sigmoid(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * 1.4426950408889634f));
+}
+#else
 __device__ __forceinline__ float cgc_softplus(float z) { return z > 20.0f ? z : log1pf(expf(z)); }
 __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + expf(-z)); }
+#endif
 
 // Forward: a receiver's in-edges are taken CGC_EB at a time: their sender indices are
 // wave-uniform (one scalar load batch), and every lane issues the batch's gathers of Ps[s] and
@@ -190,4 +206,169 @@ __global__ __launch_bounds__(256) void cgc_bwd_kernel(
       gr[(size_t)node * D2 + lane + 64 * k] = av[k];
       gr[(size_t)node * D2 + D + lane + 64 * k] = am[k];
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Receiver-streaming form (round 5, the models' factored-edge path): a wave owns CGC_RPW
+// consecutive receivers and walks their edges (one contiguous CSR range) in batches of CGC_SB,
+// the next batch's sender ids, edge-feature rows and Ps gathers in flight while the current one
+// computes; the receivers' Pr rows (and grad rows in the backward) are loaded once up front.  A
+// receiver's sum is flushed when the walk crosses its end (wave-uniform), receivers without
+// edges get 0.  Per receiver the one-wave form paid three dependent memory round trips (row
+// pointer, senders, gathers) for about four edges; here a wave pays about one per batch.
+// ---------------------------------------------------------------------------------------------
+#ifndef CGC_RPW
+#define CGC_RPW 8
+#endif
+#ifndef CGC_SB
+#define CGC_SB 8
+#endif
+static_assert(CGC_SB * CGC_EFW <= 64, "a batch's edge-feature rows are one vector load");
+
+template <int CPL>
+struct CgcBatch {
+  float zv[CGC_SB][CPL], zm[CGC_SB][CPL];   // Ps[s] gathers
+  float efv;                                 // lane l: ef row (l / 8) of the batch, column l % 8
+  int rc[CGC_SB];                            // receivers of the batch's edges (wave-uniform)
+};
+
+template <int CPL>
+__device__ __forceinline__ void cgc_batch_load(CgcBatch<CPL>& b, const float* __restrict__ ps,
+                                               const float* __restrict__ ef, const int* __restrict__ sender,
+                                               const int* __restrict__ receiver, int eb, int e1, int D,
+                                               int lane) {
+  const int D2 = 2 * D;
+#pragma unroll
+  for (int j = 0; j < CGC_SB; ++j) {
+    const int e = min(eb + j, e1 - 1);
+    const int s = sender[e];                 // wave-uniform (scalar load)
+    b.rc[j] = receiver[e];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = min(lane + 64 * k, D - 1);
+      b.zv[j][k] = ps[(size_t)s * D2 + c];
+      b.zm[j][k] = ps[(size_t)s * D2 + D + c];
+    }
+  }
+  b.efv = ef[(size_t)min(eb + (lane >> 3), e1 - 1) * CGC_EFW + (lane & 7)];
+}
+
+template <int CPL>
+__device__ __forceinline__ void cgc_batch_proj(const CgcBatch<CPL>& b, int j,
+                                               const float (&av)[CGC_EFN][CPL], const float (&am)[CGC_EFN][CPL],
+                                               float (&pv)[CPL], float (&pm)[CPL]) {
+  float f[CGC_EFN];
+#pragma unroll
+  for (int i = 0; i < CGC_EFN; ++i)
+    f[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b.efv), j * CGC_EFW + i));
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    float v = 0.0f, m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < CGC_EFN; ++i) { v = fmaf(f[i], av[i][k], v); m = fmaf(f[i], am[i][k], m); }
+    pv[k] = v;
+    pm[k] = m;
+  }
+}
+
+template <int CPL, bool BWD>
+__global__ __launch_bounds__(256) void cgc_stream_kernel(
+    const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ef,
+    const float* __restrict__ ea, const int* __restrict__ sender, const int* __restrict__ receiver,
+    const int* __restrict__ rowptr, const float* __restrict__ row_scale, int n_nodes, int D,
+    float* __restrict__ agg, const float* __restrict__ gagg, float* __restrict__ dz,
+    float* __restrict__ gr) {
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int r0 = wid * CGC_RPW;
+  if (r0 >= n_nodes) return;
+  const int nr = min(CGC_RPW, n_nodes - r0);
+  const int D2 = 2 * D;
+  const int e0 = rowptr[r0], e1 = rowptr[r0 + nr];
+  float av[CGC_EFN][CPL], am[CGC_EFN][CPL];
+  cgc_load_a<CPL, true>(ea, D, lane, av, am);
+  // the receivers' Pr rows (and grad rows, pre-scaled; the row scale in the forward), loaded once
+  float rvs[CGC_RPW][CPL], rms[CGC_RPW][CPL], gs[CGC_RPW][CPL];
+#pragma unroll
+  for (int k = 0; k < CGC_RPW; ++k) {
+    const int r = r0 + min(k, nr - 1);
+    const float sc = row_scale ? row_scale[r] : 1.0f;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = min(lane + 64 * q, D - 1);
+      rvs[k][q] = pr[(size_t)r * D2 + c];
+      rms[k][q] = pr[(size_t)r * D2 + D + c];
+      gs[k][q] = BWD ? gagg[(size_t)r * D + c] * sc : sc;
+    }
+  }
+  int cur = 0;                                   // receiver being summed (relative to r0)
+  float a1[CPL], a2[CPL];                        // fwd: message sum; bwd: sums of dz (v, m)
+  float rvc[CPL], rmc[CPL], gc[CPL];             // the current receiver's rows
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    a1[q] = 0.0f; a2[q] = 0.0f;
+    rvc[q] = rvs[0][q]; rmc[q] = rms[0][q]; gc[q] = gs[0][q];
+  }
+#define CGC_FLUSH_AND_NEXT()                                                                    \
+  {                                                                                             \
+    if (cur < nr) {                                                                             \
+      _Pragma("unroll") for (int q = 0; q < CPL; ++q) if (lane + 64 * q < D) {                  \
+        if (BWD) {                                                                              \
+          gr[(size_t)(r0 + cur) * D2 + lane + 64 * q] = a1[q];                                  \
+          gr[(size_t)(r0 + cur) * D2 + D + lane + 64 * q] = a2[q];                              \
+        } else {                                                                                \
+          agg[(size_t)(r0 + cur) * D + lane + 64 * q] = a1[q] * gc[q];                          \
+        }                                                                                       \
+      }                                                                                         \
+    }                                                                                           \
+    ++cur;                                                                                      \
+    _Pragma("unroll") for (int q = 0; q < CPL; ++q) {                                           \
+      a1[q] = 0.0f; a2[q] = 0.0f;                                                               \
+      _Pragma("unroll") for (int kk = 1; kk < CGC_RPW; ++kk) if (cur == kk) {                   \
+        rvc[q] = rvs[kk][q]; rmc[q] = rms[kk][q]; gc[q] = gs[kk][q];                            \
+      }                                                                                         \
+    }                                                                                           \
+  }
+#define CGC_PROCESS(B, EB)                                                                      \
+  _Pragma("unroll") for (int j = 0; j < CGC_SB; ++j) {                                          \
+    const int e = (EB) + j;                                                                     \
+    if (e < e1) {                                                                               \
+      const int k = B.rc[j] - r0;                                                               \
+      while (cur < k) CGC_FLUSH_AND_NEXT();                                                     \
+      float pv[CPL], pm[CPL];                                                                   \
+      cgc_batch_proj<CPL>(B, j, av, am, pv, pm);                                                \
+      _Pragma("unroll") for (int q = 0; q < CPL; ++q) {                                         \
+        const float z1 = (B.zv[j][q] + pv[q]) + rvc[q];                                         \
+        const float z2 = (B.zm[j][q] + pm[q]) + rmc[q];                                         \
+        if (!BWD) {                                                                             \
+          a1[q] += cgc_softplus(z1) * cgc_sigmoid(z2);                                          \
+        } else {                                                                                \
+          const float sv = z1 > 20.0f ? 1.0f : cgc_sigmoid(z1);                                 \
+          const float sm = cgc_sigmoid(z2);                                                     \
+          const float dv = gc[q] * sv * sm;                                                     \
+          const float dm = gc[q] * cgc_softplus(z1) * sm * (1.0f - sm);                         \
+          if (lane + 64 * q < D) {                                                              \
+            dz[(size_t)e * D2 + lane + 64 * q] = dv;                                            \
+            dz[(size_t)e * D2 + D + lane + 64 * q] = dm;                                        \
+          }                                                                                     \
+          a1[q] += dv;                                                                          \
+          a2[q] += dm;                                                                          \
+        }                                                                                       \
+      }                                                                                         \
+    }                                                                                           \
+  }
+  // two batch buffers, named (not indexed by a runtime slot: that would live in scratch)
+  CgcBatch<CPL> b0, b1;
+  if (e0 < e1) cgc_batch_load<CPL>(b0, ps, ef, sender, receiver, e0, e1, D, lane);
+  for (int eb = e0; eb < e1; eb += 2 * CGC_SB) {
+    if (eb + CGC_SB < e1) cgc_batch_load<CPL>(b1, ps, ef, sender, receiver, eb + CGC_SB, e1, D, lane);
+    CGC_PROCESS(b0, eb);
+    if (eb + CGC_SB >= e1) break;
+    if (eb + 2 * CGC_SB < e1) cgc_batch_load<CPL>(b0, ps, ef, sender, receiver, eb + 2 * CGC_SB, e1, D, lane);
+    CGC_PROCESS(b1, eb + CGC_SB);
+  }
+  // the last receiver with edges and every trailing receiver without
+  while (cur < CGC_RPW) CGC_FLUSH_AND_NEXT();
+#undef CGC_PROCESS
+#undef CGC_FLUSH_AND_NEXT
 }

@@ -113,7 +113,8 @@ class _CGCConvEF(torch.autograd.Function):
         tok = ops.TIMER.start("cgc_fwd")
         _lib.check(_lib.load().eelg_cgc_fwd_ef(
             _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
-            _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(agg), _lib.stream(agg)), "cgc_fwd_ef")
+            _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(agg),
+            _lib.stream(agg)), "cgc_fwd_ef")
         ops.TIMER.stop(tok)
         ctx.save_for_backward(x, ea, ef, ps, pr, w, row_scale)
         ctx.csr = csr
@@ -130,8 +131,8 @@ class _CGCConvEF(torch.autograd.Function):
         tok = ops.TIMER.start("cgc_bwd")
         _lib.check(_lib.load().eelg_cgc_bwd_ef(
             _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
-            _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(g), _lib.ptr(dz), _lib.ptr(gr),
-            _lib.stream(g)), "cgc_bwd_ef")
+            _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(g),
+            _lib.ptr(dz), _lib.ptr(gr), _lib.stream(g)), "cgc_bwd_ef")
         ops.TIMER.stop(tok)
         gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)
         dws, dwr, db = _cgc_dw(x, gs, gr, True)

@@ -184,13 +184,17 @@ int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* s
  * per-edge inputs with one Linear, cgc_modified.py:71-74 / cgc_vanilla.py:60-63, so
  * Ep = [e5 | 1] A): ef[E, 8] = [e5 | 1 | 0 | 0] in CSR edge order and ea[8, 2D] (rows 0..5:
  * A = [W5^T W_e^T ; b5 W_e^T], rows 6..7 unused) replace ep[E, 2D]; the kernels form Ep in
- * registers.  Same outputs as eelg_cgc_fwd / eelg_cgc_bwd on Ep = ef[:, :6] @ ea[:6]. */
+ * registers.  Same outputs as eelg_cgc_fwd / eelg_cgc_bwd on Ep = ef[:, :6] @ ea[:6].
+ * receiver[E] (the CSR's receiver of each sorted edge; may be NULL) enables the receiver-
+ * streaming kernels: a wave walks the edges of 8 consecutive receivers in batches of 8, the
+ * next batch's loads in flight (EELG_CGC_STREAM bit 0 forward, bit 1 backward; default 2). */
 int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
-                    const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
-                    int D, float* agg, void* stream);
+                    const int* sender, const int* receiver, const int* rowptr,
+                    const float* row_scale, int n_nodes, int D, float* agg, void* stream);
 int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
-                    const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
-                    int D, const float* grad_agg, float* dz, float* grad_pr, void* stream);
+                    const int* sender, const int* receiver, const int* rowptr,
+                    const float* row_scale, int n_nodes, int D, const float* grad_agg, float* dz,
+                    float* grad_pr, void* stream);
 
 /* Sparse (CSR) x dense with strided operands:
  * out[r*ldo_r + c*ldo_c] = sum_{j in row r} val[j] * B[col[j]*ldb_r + c*ldb_c].
