@@ -708,10 +708,12 @@ static int cgc_stream_mask() {
 }
 static bool cgc_stream(bool bwd) { return (cgc_stream_mask() >> (bwd ? 1 : 0)) & 1; }
 
+static_assert(CGC_RPW == EELG_CGC_RPW, "eelg.h EELG_CGC_RPW");
 static int cgc_launch_stream(bool bwd, const float* ps, const float* pr, const float* ef,
                              const float* ea, const int* sender, const int* receiver, const int* rowptr,
                              const float* row_scale, int n_nodes, int D, float* agg,
-                             const float* grad_agg, float* dz, float* grad_pr, void* stream) {
+                             const float* grad_agg, float* dz, float* grad_pr, float* dea_part,
+                             void* stream) {
   if (D <= 0) return fail(-2, "cgc_stream: D must be positive");
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_stream: D = %d > %d not built", D, EELG_CGC_MAXD);
@@ -720,7 +722,7 @@ static int cgc_launch_stream(bool bwd, const float* ps, const float* pr, const f
   hipStream_t st = (hipStream_t)stream;
 #define CGCS(C, B) hipLaunchKernelGGL((cgc_stream_kernel<C, B>), g, dim3(256), 0, st, ps, pr, ef, ea, \
                                       sender, receiver, rowptr, row_scale, n_nodes, D, agg, grad_agg, \
-                                      dz, grad_pr)
+                                      dz, grad_pr, dea_part)
   const int cpl = D > 128 ? 4 : D > 64 ? 2 : 1;
   if (bwd) { if (cpl == 4) CGCS(4, true); else if (cpl == 2) CGCS(2, true); else CGCS(1, true); }
   else { if (cpl == 4) CGCS(4, false); else if (cpl == 2) CGCS(2, false); else CGCS(1, false); }
@@ -734,18 +736,24 @@ int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const flo
   if (!ef || !ea) return fail(-2, "cgc_fwd_ef: ef and ea are required");
   if (cgc_stream(false) && receiver)
     return cgc_launch_stream(false, ps, pr, ef, ea, sender, receiver, rowptr, row_scale, n_nodes, D,
-                             agg, nullptr, nullptr, nullptr, stream);
+                             agg, nullptr, nullptr, nullptr, nullptr, stream);
   return cgc_launch_fwd(ps, pr, nullptr, ef, ea, sender, rowptr, row_scale, n_nodes, D, agg, stream);
+}
+
+int eelg_cgc_bwd_ef_parts(int n_nodes) {
+  const int waves = (n_nodes + EELG_CGC_RPW - 1) / EELG_CGC_RPW;
+  return n_nodes > 0 ? (waves + 3) / 4 : 0;
 }
 
 int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
                     const int* sender, const int* receiver, const int* rowptr,
                     const float* row_scale, int n_nodes, int D, const float* grad_agg, float* dz,
-                    float* grad_pr, void* stream) {
+                    float* grad_pr, float* dea_part, void* stream) {
   if (!ef || !ea) return fail(-2, "cgc_bwd_ef: ef and ea are required");
-  if (cgc_stream(true) && receiver)
+  if (dea_part && !receiver) return fail(-2, "cgc_bwd_ef: dea_part needs the receiver array");
+  if ((cgc_stream(true) || dea_part) && receiver)
     return cgc_launch_stream(true, ps, pr, ef, ea, sender, receiver, rowptr, row_scale, n_nodes, D,
-                             nullptr, grad_agg, dz, grad_pr, stream);
+                             nullptr, grad_agg, dz, grad_pr, dea_part, stream);
   return cgc_launch_bwd(ps, pr, nullptr, ef, ea, sender, rowptr, row_scale, n_nodes, D, grad_agg,
                         dz, grad_pr, stream);
 }

@@ -254,13 +254,16 @@ __device__ __forceinline__ void cgc_batch_load(CgcBatch<CPL>& b, const float* __
 }
 
 template <int CPL>
-__device__ __forceinline__ void cgc_batch_proj(const CgcBatch<CPL>& b, int j,
-                                               const float (&av)[CGC_EFN][CPL], const float (&am)[CGC_EFN][CPL],
-                                               float (&pv)[CPL], float (&pm)[CPL]) {
-  float f[CGC_EFN];
+__device__ __forceinline__ void cgc_batch_feat(const CgcBatch<CPL>& b, int j, float (&f)[CGC_EFN]) {
 #pragma unroll
   for (int i = 0; i < CGC_EFN; ++i)
     f[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b.efv), j * CGC_EFW + i));
+}
+
+template <int CPL>
+__device__ __forceinline__ void cgc_batch_proj(const float (&f)[CGC_EFN],
+                                               const float (&av)[CGC_EFN][CPL], const float (&am)[CGC_EFN][CPL],
+                                               float (&pv)[CPL], float (&pm)[CPL]) {
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     float v = 0.0f, m = 0.0f;
@@ -277,21 +280,28 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
     const float* __restrict__ ea, const int* __restrict__ sender, const int* __restrict__ receiver,
     const int* __restrict__ rowptr, const float* __restrict__ row_scale, int n_nodes, int D,
     float* __restrict__ agg, const float* __restrict__ gagg, float* __restrict__ dz,
-    float* __restrict__ gr) {
+    float* __restrict__ gr, float* __restrict__ dea_part) {
   const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int r0 = wid * CGC_RPW;
-  if (r0 >= n_nodes) return;
-  const int nr = min(CGC_RPW, n_nodes - r0);
+  // a wave past the last receiver still takes part in the workgroup's reduction of the
+  // edge-factor gradient at the end (with zeros)
+  const int nr = max(0, min(CGC_RPW, n_nodes - r0));
   const int D2 = 2 * D;
-  const int e0 = rowptr[r0], e1 = rowptr[r0 + nr];
+  const int e0 = nr > 0 ? rowptr[r0] : 0, e1 = nr > 0 ? rowptr[r0 + nr] : 0;
   float av[CGC_EFN][CPL], am[CGC_EFN][CPL];
   cgc_load_a<CPL, true>(ea, D, lane, av, am);
+  // backward: d ea[i][k] = sum over the wave's edges of ef[e][i] * dz[e][k] (rows 0..5)
+  float dav[CGC_EFN][CPL], dam[CGC_EFN][CPL];
+#pragma unroll
+  for (int i = 0; i < CGC_EFN; ++i)
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) { dav[i][q] = 0.0f; dam[i][q] = 0.0f; }
   // the receivers' Pr rows (and grad rows, pre-scaled; the row scale in the forward), loaded once
   float rvs[CGC_RPW][CPL], rms[CGC_RPW][CPL], gs[CGC_RPW][CPL];
 #pragma unroll
   for (int k = 0; k < CGC_RPW; ++k) {
-    const int r = r0 + min(k, nr - 1);
+    const int r = min(r0 + min(k, nr - 1), n_nodes - 1);
     const float sc = row_scale ? row_scale[r] : 1.0f;
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
@@ -335,8 +345,9 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
     if (e < e1) {                                                                               \
       const int k = B.rc[j] - r0;                                                               \
       while (cur < k) CGC_FLUSH_AND_NEXT();                                                     \
-      float pv[CPL], pm[CPL];                                                                   \
-      cgc_batch_proj<CPL>(B, j, av, am, pv, pm);                                                \
+      float pv[CPL], pm[CPL], f_[CGC_EFN];                                                      \
+      cgc_batch_feat<CPL>(B, j, f_);                                                            \
+      cgc_batch_proj<CPL>(f_, av, am, pv, pm);                                                  \
       _Pragma("unroll") for (int q = 0; q < CPL; ++q) {                                         \
         const float z1 = (B.zv[j][q] + pv[q]) + rvc[q];                                         \
         const float z2 = (B.zm[j][q] + pm[q]) + rmc[q];                                         \
@@ -353,6 +364,10 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
           }                                                                                     \
           a1[q] += dv;                                                                          \
           a2[q] += dm;                                                                          \
+          _Pragma("unroll") for (int i = 0; i < CGC_EFN; ++i) {                                 \
+            dav[i][q] = fmaf(f_[i], dv, dav[i][q]);                                             \
+            dam[i][q] = fmaf(f_[i], dm, dam[i][q]);                                             \
+          }                                                                                     \
         }                                                                                       \
       }                                                                                         \
     }                                                                                           \
@@ -371,4 +386,27 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
   while (cur < CGC_RPW) CGC_FLUSH_AND_NEXT();
 #undef CGC_PROCESS
 #undef CGC_FLUSH_AND_NEXT
+  if (BWD && dea_part) {
+    // the workgroup's partial of d ea: the 4 waves' sums added through LDS in wave order
+    __shared__ float red[4 * CGC_EFN * 2 * 64 * CPL];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < CGC_EFN; ++i)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        red[((w * CGC_EFN + i) * 2 + 0) * 64 * CPL + q * 64 + lane] = dav[i][q];
+        red[((w * CGC_EFN + i) * 2 + 1) * 64 * CPL + q * 64 + lane] = dam[i][q];
+      }
+    __syncthreads();
+    float* __restrict__ dst = dea_part + (size_t)blockIdx.x * CGC_EFN * D2;
+    for (int t = threadIdx.x; t < CGC_EFN * 2 * 64 * CPL; t += 256) {
+      const int i = t / (2 * 64 * CPL), rem = t - i * 2 * 64 * CPL;
+      const int half = rem / (64 * CPL), c = rem - half * 64 * CPL;   // c = q * 64 + lane
+      float v = 0.0f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) v += red[((ww * CGC_EFN + i) * 2 + half) * 64 * CPL + c];
+      const int ch = (c & 63) + 64 * (c >> 6);                         // channel lane + 64 q
+      if (ch < D) dst[i * D2 + half * D + ch] = v;
+    }
+  }
 }

@@ -1460,15 +1460,31 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
                 expr = v if expr is None else f"(a_ >= {a0} ? {v} : {expr})"
             return expr
         # a rolled loop: its per-row address arithmetic stays inside (unrolled, the uniform row
-        # values were hoisted to the kernel top and spilled SGPRs in grad-x)
+        # values were hoisted to the kernel top and spilled SGPRs in grad-x).  Four consecutive
+        # nodes per iteration leave as one float4 when the rows are 16-B aligned (n_nodes % 4 == 0,
+        # the tile start is a multiple of 64): round 5, a quarter of the store instructions
+        q4 = nb // 4
+        sh4 = q4.bit_length() - 1
         out = ["{ int tid_ = threadIdx.x; asm volatile(\"\" : \"+v\"(tid_));",
+               "  const bool v4_ = (n_nodes & 3) == 0;",
                "#pragma unroll 1",
-               f"  for (int i_ = tid_; i_ < {tot}; i_ += {nth}) {{",
-               f"    const int row_ = i_ >> {sh}, nl_ = i_ & {nb - 1};",
+               f"  for (int i_ = tid_; i_ < {tot // 4}; i_ += {nth}) {{",
+               f"    const int row_ = i_ >> {sh4}, nl_ = (i_ & {q4 - 1}) * 4;",
                f"    const int cl_ = row_ / {dd}, a_ = row_ - cl_ * {dd};",
-               f"    if (n0 + nl_ < n_nodes) {dst}[(size_t)((cq * {Q} + cl_) * {dd} + a_) * n_nodes + n0 + nl_] = "
-               f"{tile}[nl_ * {TP} + {col()}];",
+               f"    const int c_ = {col()};",
+               f"    float* __restrict__ d_ = {dst} + (size_t)((cq * {Q} + cl_) * {dd} + a_) * n_nodes + n0 + nl_;",
+               f"    const float t0_ = {tile}[nl_ * {TP} + c_], t1_ = {tile}[(nl_ + 1) * {TP} + c_],",
+               f"                t2_ = {tile}[(nl_ + 2) * {TP} + c_], t3_ = {tile}[(nl_ + 3) * {TP} + c_];",
+               "    if (v4_ && n0 + nl_ + 3 < n_nodes) {",
+               "      *reinterpret_cast<float4*>(d_) = make_float4(t0_, t1_, t2_, t3_);",
+               "    } else {",
+               "      if (n0 + nl_ < n_nodes) d_[0] = t0_;",
+               "      if (n0 + nl_ + 1 < n_nodes) d_[1] = t1_;",
+               "      if (n0 + nl_ + 2 < n_nodes) d_[2] = t2_;",
+               "      if (n0 + nl_ + 3 < n_nodes) d_[3] = t3_;",
+               "    }",
                "  }", "}"]
+        assert tot % 4 == 0 and nb % 4 == 0
         return [ind + ln for ln in out]
 
     # group terms by (a, b) pair

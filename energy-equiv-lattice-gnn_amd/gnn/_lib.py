@@ -46,7 +46,8 @@ _SIGS = {
     "eelg_cgc_fwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_cgc_bwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_cgc_fwd_ef": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),
-    "eelg_cgc_bwd_ef": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
+    "eelg_cgc_bwd_ef": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P], _I),
+    "eelg_cgc_bwd_ef_parts": ([_I], _I),
     "eelg_csr_spmm": ([_P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P], _I),
     "eelg_sc_fwd": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),

@@ -45,19 +45,36 @@ def as_csr(edge_index: EdgeIndex, num_nodes: int, *edge_tensors):
     return (csr,) + tuple(t[csr.perm] for t in edge_tensors)
 
 
+def mat_square(c: torch.Tensor) -> torch.Tensor:
+    """``c @ c`` for a batch of small (6 x 6) matrices as broadcast products and a sum: the
+    library batched GEMM launches several 16x16-tile kernels (and two more in the backward) for
+    what is 216 multiply-adds per matrix"""
+    return (c.unsqueeze(-1) * c.unsqueeze(-3)).sum(-2)
+
+
+def mat_power(c: torch.Tensor, k: int) -> torch.Tensor:
+    """``torch.linalg.matrix_power(c, k)`` for k in {2, 4} by repeated ``mat_square``"""
+    if k == 2:
+        return mat_square(c)
+    if k == 4:
+        return mat_square(mat_square(c))
+    return torch.linalg.matrix_power(c, k)
+
+
 class PositiveLayer(torch.nn.Module):
-    """``gnn/blocks.py:185-229``."""
+    """``gnn/blocks.py:185-229``; the matrix powers as ``mat_power`` (same products, elementwise
+    kernels instead of library GEMMs)."""
 
     def __init__(self, params: Namespace):
         super().__init__()
         f = params.positive_function
         eye = lambda c: torch.eye(6, device=c.device, dtype=c.dtype)  # noqa: E731
         funcs = {
-            "matrix_power_2": lambda c: torch.linalg.matrix_power(c, 2),
-            "matrix_power_4": lambda c: torch.linalg.matrix_power(c, 4),
+            "matrix_power_2": lambda c: mat_power(c, 2),
+            "matrix_power_4": lambda c: mat_power(c, 4),
             "matrix_exp": torch.linalg.matrix_exp,
-            "matrix_trunc_exp_2": lambda c: torch.linalg.matrix_power(eye(c) + c / 2, 2),
-            "matrix_trunc_exp_4": lambda c: torch.linalg.matrix_power(eye(c) + c / 4, 4),
+            "matrix_trunc_exp_2": lambda c: mat_power(eye(c) + c / 2, 2),
+            "matrix_trunc_exp_4": lambda c: mat_power(eye(c) + c / 4, 4),
             "none": lambda c: c,
         }
         if f not in funcs:

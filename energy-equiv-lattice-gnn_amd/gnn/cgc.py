@@ -20,7 +20,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib, dense, ops
-from .blocks import EdgeIndex, as_csr
+from .blocks import EdgeIndex, as_csr, mat_square
 
 # Mandel 6x6 from the 21 upper-triangular outputs (cgc_modified.py:28-33)
 INDS_VAL = [[0, 1, 2, 3, 4, 5],
@@ -128,15 +128,20 @@ class _CGCConvEF(torch.autograd.Function):
         g = ops._f32(g).contiguous()
         dz = torch.empty(csr.num_edges, 2 * d, device=x.device, dtype=torch.float32)
         gr = torch.empty(n, 2 * d, device=x.device, dtype=torch.float32)
+        lib = _lib.load()
+        nparts = int(lib.eelg_cgc_bwd_ef_parts(n))
+        dea_part = torch.empty(nparts, 6, 2 * d, device=x.device, dtype=torch.float32)
         tok = ops.TIMER.start("cgc_bwd")
-        _lib.check(_lib.load().eelg_cgc_bwd_ef(
+        _lib.check(lib.eelg_cgc_bwd_ef(
             _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
             _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(g),
-            _lib.ptr(dz), _lib.ptr(gr), _lib.stream(g)), "cgc_bwd_ef")
+            _lib.ptr(dz), _lib.ptr(gr), _lib.ptr(dea_part), _lib.stream(g)), "cgc_bwd_ef")
         ops.TIMER.stop(tok)
         gs = ops.segment_sum_csr(dz, csr.srowptr, n, idx=csr.sperm)
         dws, dwr, db = _cgc_dw(x, gs, gr, True)
-        dea = dense.linear_bwd_w(ef, dz).t()                      # [8, 2D] = ef^T dz
+        # d ea = ef^T dz: the kernel's per-workgroup partials (rows 0..5), summed in a fixed order
+        dea = torch.cat([ops.sum_rows(dea_part) if nparts else dea_part.new_zeros(6, 2 * d),
+                         dea_part.new_zeros(2, 2 * d)])
         zero = torch.zeros(2 * d, d, device=x.device, dtype=torch.float32)
         dw = torch.cat([dws, dwr, zero], dim=1)                   # the edge block: through ea
         dx = _cgc_dx(gs, gr, w, d)
@@ -262,7 +267,7 @@ class CrystGraphConv(_CGCBase):
             h = h + self._layer(i, h, csr, ef)
         a = self.mlp(self._pool(h, batch))[:, self.inds_val]
         if self.params.positive == "square":
-            return {"stiffness": torch.linalg.matrix_power(a, 2)}
+            return {"stiffness": mat_square(a)}
         if self.params.positive == "none":
             return {"stiffness": a}
         raise NotImplementedError(self.params.positive)

@@ -194,7 +194,12 @@ int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const flo
 int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
                     const int* sender, const int* receiver, const int* rowptr,
                     const float* row_scale, int n_nodes, int D, const float* grad_agg, float* dz,
-                    float* grad_pr, void* stream);
+                    float* grad_pr, float* dea_part, void* stream);
+/* dea_part (may be NULL; needs receiver): per-workgroup partials [eelg_cgc_bwd_ef_parts(n), 6, 2D]
+ * of d ea[0..5] = ef[:, :6]^T dz, summed by the caller (deterministic); a workgroup covers
+ * 4 * EELG_CGC_RPW receivers. */
+#define EELG_CGC_RPW 8
+int eelg_cgc_bwd_ef_parts(int n_nodes);
 
 /* Sparse (CSR) x dense with strided operands:
  * out[r*ldo_r + c*ldo_c] = sum_{j in row r} val[j] * B[col[j]*ldb_r + c*ldb_c].
