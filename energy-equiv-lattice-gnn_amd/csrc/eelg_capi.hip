@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
+#include <vector>
 
 #include "../../include/eelg.h"
 #include "eelg_internal.h"
@@ -427,6 +428,32 @@ static int segment_sum_launch(const T* src, const int* rowptr, const int* idx,
   return check_launch(what);
 }
 
+const eelg_tp_cfg* eelg_tp_table(int* n) {
+  // the per-mul tables concatenated once (thread-safe static initialisation)
+  static const std::vector<eelg_tp_cfg> all = [] {
+    std::vector<eelg_tp_cfg> v;
+    for (auto get : {eelg_tp_table_m32, eelg_tp_table_m16, eelg_tp_table_m64}) {
+      int k = 0;
+      const eelg_tp_cfg* t = get(&k);
+      v.insert(v.end(), t, t + k);
+    }
+    return v;
+  }();
+  *n = (int)all.size();
+  return all.data();
+}
+
+const eelg_sc_cfg* eelg_sc_table(int* n) { return eelg_sc_table_m32(n); }
+
+const eelg_sc_cfg* eelg_sc_table_mul(int mul, int* n) {
+  switch (mul) {
+    case 16: return eelg_sc_table_m16(n);
+    case 32: return eelg_sc_table_m32(n);
+    case 64: return eelg_sc_table_m64(n);
+    default: *n = 0; return nullptr;
+  }
+}
+
 extern "C" {
 
 const char* eelg_version(void) { return EELG_VERSION; }
@@ -520,6 +547,7 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
                      const int* rowptr, int n_nodes, float inv_norm, float* agg, void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
+  if (!c->fwd_bf) return fail(-2, "tp_fwd_bf16: bf16 storage is generated for mul 32 only (config %s)", c->name);
   if (n_nodes <= 0) return 0;
   // LDS-DMA pieces of 16 B, as the fp32 kernel (bf16 weight rows are wn * 2 B, a multiple of 16)
   if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(sh) |
@@ -556,6 +584,7 @@ int eelg_tp_bwd_sorted_bf16(int cfg, const float* x, const float* sh, const void
                             void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
+  if (!c->bwd_bf) return fail(-2, "tp_bwd_bf16: bf16 storage is generated for mul 32 only (config %s)", c->name);
   if (n_edges <= 0) return 0;
   hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sender,
@@ -591,6 +620,7 @@ int eelg_tp_bwd_sender_bf16(int cfg, const float* x, const float* sh, const void
                             float* grad_x, void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
+  if (!c->bws_bf) return fail(-2, "tp_bwd_sender_bf16: bf16 storage is generated for mul 32 only (config %s)", c->name);
   if (n_nodes <= 0) return 0;
   hipLaunchKernelGGL(c->bws_bf, dim3((n_nodes + 7) / 8, c->nbgroups), dim3(256), 0,
                      (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sperm,
@@ -769,9 +799,9 @@ int eelg_csr_spmm(const int* rowptr, const int* col, const float* val, int n_row
 
 static const eelg_sc_cfg* sc_get(int cfg, int mul) {
   int n = 0;
-  const eelg_sc_cfg* t = eelg_sc_table(&n);
+  const eelg_sc_cfg* t = eelg_sc_table_mul(mul, &n);
+  if (!t) { fail(-2, "symmetric contraction built for mul 16 / 32 / 64, got %d", mul); return nullptr; }
   if (cfg < 0 || cfg >= n) { fail(-1, "bad sc config %d", cfg); return nullptr; }
-  if (mul != 32) { fail(-2, "symmetric contraction built for mul=32, got %d", mul); return nullptr; }
   return &t[cfg];
 }
 

@@ -56,7 +56,12 @@ struct eelg_sc_cfg {
   int cld;                       // coefficient row stride (nterms rounded up to 16: 64-B aligned rows)
 };
 
+// every generated tensor-product set, all channel counts (eelg_capi.hip merges the per-mul tables
+// of the generated translation units: generated/eelg_gen.hip for mul 32, eelg_gen_m16 / _m64)
 const eelg_tp_cfg* eelg_tp_table(int* n);
+const eelg_tp_cfg* eelg_tp_table_m16(int* n);
+const eelg_tp_cfg* eelg_tp_table_m32(int* n);
+const eelg_tp_cfg* eelg_tp_table_m64(int* n);
 
 // error reporting shared by the translation units of libeelg.so (eelg_capi.hip)
 int eelg_fail(int code, const char* fmt, ...);
@@ -68,7 +73,13 @@ __device__ __forceinline__ float eelg_bf2f(unsigned short v) { return __uint_as_
 __device__ __forceinline__ unsigned short eelg_f2bf(float f) {
   return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
+// symmetric-contraction sets: one table per channel count, the same configs in the same order
+// (eelg_sc_table = the mul-32 table; eelg_sc_table_mul: nullptr for a mul that was not generated)
 const eelg_sc_cfg* eelg_sc_table(int* n);
+const eelg_sc_cfg* eelg_sc_table_mul(int mul, int* n);
+const eelg_sc_cfg* eelg_sc_table_m16(int* n);
+const eelg_sc_cfg* eelg_sc_table_m32(int* n);
+const eelg_sc_cfg* eelg_sc_table_m64(int* n);
 
 // fp32-accurate GEMM operands on bf16 MFMA ("x6"): an fp32 value splits EXACTLY into three bf16
 // parts by truncation, x = p0 + p1 + p2 (p0 = the top 8 significant bits, p1 the next 8 of the

@@ -132,9 +132,9 @@ def tp_configs() -> Dict[str, Tuple[Irreps, Irreps, Irreps]]:
     for lmax in kernel_sets.LMAX:
         sh = Irreps.spherical_harmonics(lmax)
         target = (sh * MUL).sort()[0].simplify()
-        assert str(target) == kernel_sets.coupling_target(lmax)
+        assert str(target) == kernel_sets.coupling_target(lmax, MUL)
         out[f"tpA_l{lmax}"] = (Irreps(f"{MUL}x0e"), sh, target)
-        out[f"tpB_l{lmax}"] = (hidden_irreps(lmax), sh, target)
+        out[f"tpB_l{lmax}"] = (hidden_irreps(lmax, MUL), sh, target)
     return out
 
 
@@ -316,10 +316,18 @@ def sh_load(need_l2: Sequence[int], pref: str, base: str) -> List[str]:
     return out
 
 
-def _glds_chunks(groups, nshp, node_off, wes: int = 4):
+def _chan_groups():
+    """(channel groups, lanes per group) of the interaction kernels: a half-wave computes 32
+    channels of one receiver / edge, so mul = 64 runs as two channel groups and mul = 16 as one
+    group whose lanes 16..31 compute nothing that is stored"""
+    return max(1, MUL // 32), min(MUL, 32)
+
+
+def _glds_chunks(groups, nshp, node_off, wes: int = 4, cg: int = 0):
     """Per path group: the 16-B chunk list of one half-wave's rows for one edge (x blocks of
     x[sender], the SH row, the group's weight slices of ``wes`` bytes per weight) and the image
-    offsets in 4-byte units."""
+    offsets in 4-byte units; ``cg`` = the channel group (its lanes' channel slice of every row)."""
+    _, LW = _chan_groups()
     glist = []
     for grp in groups:
         need_l1 = sorted({p.l1 for p in grp})
@@ -329,12 +337,12 @@ def _glds_chunks(groups, nshp, node_off, wes: int = 4):
         def add_w():
             for p in grp:
                 fo_w[p.slot] = 4 * len(chunks)
-                chunks.extend((2, wes * p.slot * MUL + 16 * cc) for cc in range(wes * MUL // 16))
+                chunks.extend((2, wes * (p.slot * MUL + cg * LW) + 16 * cc) for cc in range(wes * LW // 16))
         if TP_FWD_WNT:
             add_w()
         for l in need_l1:
             fo_x[l] = 4 * len(chunks)
-            chunks += [(0, 4 * node_off[l] + 16 * cc) for cc in range(8 * (2 * l + 1))]
+            chunks += [(0, 4 * (node_off[l] + cg * LW * (2 * l + 1)) + 16 * cc) for cc in range(LW * (2 * l + 1) // 4)]
         fo_sh = 4 * len(chunks)
         chunks += [(1, 16 * cc) for cc in range(nshp // 4)]
         if not TP_FWD_WNT:
@@ -402,9 +410,10 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     its lanes."""
     WPB = TP_FWD_WPB
     TN = 2 * WPB * TP_NPH
-    ng = len(groups)
-    glist = _glds_chunks(groups, nshp, node_off, 2 if bf else 4)
-    NJ = max(-(-len(g[2]) // 64) for g in glist)
+    CG, LW = _chan_groups()
+    ng = len(groups) * CG                 # blocks per node tile: (path group, channel group)
+    glists = [_glds_chunks(groups, nshp, node_off, 2 if bf else 4, c) for c in range(CG)]
+    NJ = max(-(-len(g[2]) // 64) for gl in glists for g in gl)
     NI = NJ * 64
     L: List[str] = []
     wpe = f" __attribute__((amdgpu_waves_per_eu({TP_FWD_WPE})))" if TP_FWD_WPE else ""
@@ -416,7 +425,7 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
     L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5;")
     L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-    L.append(f"  const int u = lane & {MUL - 1};")
+    L.append("  const int u = lane & 31;")
     L.append(f"  const int ntl = (n_nodes + {TN - 1}) / {TN}, tpx = (ntl + 7) >> 3;")
     L.append(f"  const int q = blockIdx.x >> 3, grp = q % {ng};")
     L.append(f"  const int tile = (blockIdx.x & 7) * tpx + q / {ng};")
@@ -432,10 +441,12 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
         L.append(f"  int node_{h} = n0_{h}, nend_{h} = rowptr[min(n0_{h} + 1, n1_{h})], "
                  f"nend2_{h} = rowptr[min(n0_{h} + 2, n1_{h})];")
     L.append("  switch (grp) {")
-    for gi, grp in enumerate(groups):
-        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glist[gi]
+    for ci, (gi, cg) in enumerate((gi, cg) for gi in range(len(groups)) for cg in range(CG)):
+        grp = groups[gi]
+        need_l1, need_l2, chunks, fo_x, fo_sh, fo_w = glists[cg][gi]
         nj = -(-len(chunks) // 64)
-        L.append(f"  case {gi}: {{ // {len(chunks)} chunks of 16 B per half-wave and edge")
+        L.append(f"  case {ci}: {{ // {len(chunks)} chunks of 16 B per half-wave and edge"
+                 + (f", channel group {cg}" if CG > 1 else ""))
         L += _glds_desc(chunks, nj)
 
         def issue(buf, ahead):
@@ -524,12 +535,12 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
         L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
         for h in (0, 1):
             L.append(f"      while (node_{h} < n1_{h} && nend_{h} == e_{h}) {{   // uniform")
-            L.append(f"        if (hf == {h}) {{")
+            L.append(f"        if (hf == {h}{f' && u < {LW}' if LW < 32 else ''}) {{")
             L.append(f"          float* __restrict__ o = agg + (size_t)node_{h} * {dmid};")
             for p in grp:
                 d3 = 2 * p.l3 + 1
                 L.extend("          " + ln for ln in vec_store([f"a{p.slot}_{k}" for k in range(d3)], "o",
-                                                             f"{p.out_off} + u * {d3}", nt=bool(TP_FWD_ANT)))
+                                                             f"{p.out_off + cg * LW * d3} + u * {d3}", nt=bool(TP_FWD_ANT)))
             L.append("          " + " ".join(f"{a} = 0.0f;" for a in accs))
             L.append("        }")
             L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
@@ -584,6 +595,15 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     ng = len(groups)
     L += _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf)
 
+    # channel groups (mul = 64: two 32-channel groups on blockIdx.y; mul = 16: lanes 16..31 idle)
+    CG, LW = _chan_groups()
+    UC = "u" if (CG, LW) == (1, 32) else "uc"     # this lane's channel in the row layouts
+    YSW = "blockIdx.y" if CG == 1 else f"blockIdx.y / {CG}"
+    chan_head = ["  const int u = lane & 31;"]
+    if CG > 1:
+        chan_head.append(f"  const int uc = u + (blockIdx.y % {CG}) * 32;")
+    elif LW < 32:
+        chan_head += [f"  if (u >= {LW}) return;   // no channel", "  const int uc = u;"]
     # ---------------- backward (per edge) ----------------
     # grouped by input block l1: each group owns a disjoint slice of gxe, so no
     # cross-group reduction is needed; grad_w of every path is written once.
@@ -595,7 +615,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("    const float* __restrict__ gagg, float inv_norm,")
     L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe, const int* __restrict__ spos) {{")
     L.append("  const int lane = threadIdx.x & 63;")
-    L.append(f"  const int u = lane & {MUL - 1};")
+    L += chan_head
     # spos (optional): gxe row of edge e is spos[e], its position in sender order, so the sender
     # sum reads gxe contiguously instead of gathering rows through sperm
     # a half-wave streams TP_BWD_EPH consecutive edges: while the last path of edge e
@@ -605,7 +625,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append(f"  const int e0 = ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {EPH};")
     L.append("  if (e0 >= n_edges) return;")
     L.append(f"  const int e1 = min(e0 + {EPH}, n_edges);")
-    L.append("  switch (blockIdx.y) {")
+    L.append(f"  switch ({YSW}) {{")
     for gi, grp in enumerate(bgroups):
         l = grp[0].l1
         d = 2 * l + 1
@@ -621,12 +641,12 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             out = [f"    {{ const float* __restrict__ xs = x + (size_t){sv} * {din};",
                    f"      const float* __restrict__ ye = sh + (size_t){ev} * {nshp};",
                    f"      const float* __restrict__ ge = gagg + (size_t){rv} * {dmid};",
-                   f"      const {WT}* __restrict__ we = w + (size_t){ev} * {wn} + u;"]
-            out += ["      " + ln for ln in vec_load([pref + v for v in xs_], "xs", f"{node_off[l]} + u * {d}")]
+                   f"      const {WT}* __restrict__ we = w + (size_t){ev} * {wn} + {UC};"]
+            out += ["      " + ln for ln in vec_load([pref + v for v in xs_], "xs", f"{node_off[l]} + {UC} * {d}")]
             out += ["      " + ln for ln in sh_load(l2s, pref, "ye")]
             d3 = 2 * p0.l3 + 1
             out += ["      " + ln for ln in vec_load([f"{pref}g{p0.slot}_{k}" for k in range(d3)], "ge",
-                                                      f"{p0.out_off} + u * {d3}")]
+                                                      f"{p0.out_off} + {UC} * {d3}")]
             out.append(f"      {pref}w{p0.slot} = {ld_w(f'we[{p0.slot * MUL}]')};")
             out.append("    }")
             return out
@@ -639,8 +659,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             L.append("      const int sn = more ? sender[e + 1] : 0, rn = more ? receiver[e + 1] : 0;")
             L.append("      const int en = more ? e + 1 : e;")
         L.append("      const float* __restrict__ ge = gagg + (size_t)rcur * " + str(dmid) + ";")
-        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
-        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
+        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + {UC};")
+        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + {UC};")
         L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)(spos ? spos[e] : e) * {din};")
         for i in range(d):
             L.append(f"      float gx{l}_{i} = 0.0f;")
@@ -653,7 +673,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             d3 = 2 * p.l3 + 1
             out = ["      float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
             out += ["      " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
-                                                    f"{p.out_off} + u * {d3}")]
+                                                    f"{p.out_off} + {UC} * {d3}")]
             out.append(f"      float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
         PF = TP_BWD_PFD
@@ -701,9 +721,9 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             L.append("      }")
             L.append("      " + pin(base_pin + nxt_regs))
         if bf:
-            L += [f"      gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
+            L += [f"      gxo[{node_off[l]} + {UC} * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
         else:
-            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}",
+            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + {UC} * {d}",
                                                        nt=bool(TP_BWD_NT))]
         if EPH > 1:
             L.append("      " + " ".join(f"{v} = n{v};" for v in xs_ + ys_ + g0_) + " rcur = rn;")
@@ -726,11 +746,11 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("    const float* __restrict__ gagg, float inv_norm,")
     L.append(f"    {WT}* __restrict__ gw, float* __restrict__ gx) {{")
     L.append("  const int lane = threadIdx.x & 63;")
-    L.append(f"  const int u = lane & {MUL - 1};")
+    L += chan_head
     L.append("  const int n = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);")
     L.append("  if (n >= n_nodes) return;")
     L.append("  const int p0 = srowptr[n], p1 = srowptr[n + 1];")
-    L.append("  switch (blockIdx.y) {")
+    L.append(f"  switch ({YSW}) {{")
     for gi, grp in enumerate(bgroups):
         l = grp[0].l1
         d = 2 * l + 1
@@ -741,7 +761,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
         L.append(f"  case {gi}: {{ // input block l1 = {l}")
         L.append("    float " + ", ".join(xs_) + ";")
         L.append(f"    {{ const float* __restrict__ xs = x + (size_t)n * {din};")
-        L += ["      " + ln for ln in vec_load(xs_, "xs", f"{node_off[l]} + u * {d}")]
+        L += ["      " + ln for ln in vec_load(xs_, "xs", f"{node_off[l]} + {UC} * {d}")]
         L.append("    }")
         L.append("    float " + ", ".join(f"{v} = 0.0f" for v in gxs) + ";")
         L.append("    int en = p0 < p1 ? sperm[p0] : 0;")
@@ -751,8 +771,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
         L.append("      const int r = receiver[e];")
         L.append(f"      const float* __restrict__ ye = sh + (size_t)e * {nshp};")
         L.append(f"      const float* __restrict__ ge = gagg + (size_t)r * {dmid};")
-        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
-        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
+        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + {UC};")
+        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + {UC};")
         L.append("      float " + ", ".join(ys_) + ";")
         L += ["      " + ln for ln in sh_load(l2s, "", "ye")]
 
@@ -760,7 +780,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             d3 = 2 * p.l3 + 1
             out = ["      float " + ", ".join(f"g{p.slot}_{k}" for k in range(d3)) + ";"]
             out += ["      " + ln for ln in vec_load([f"g{p.slot}_{k}" for k in range(d3)], "ge",
-                                                    f"{p.out_off} + u * {d3}")]
+                                                    f"{p.out_off} + {UC} * {d3}")]
             out.append(f"      float w{p.slot} = {ld_w(f'we[{p.slot * MUL}]')};")
             return out, [f"g{p.slot}_{k}" for k in range(d3)] + [f"w{p.slot}"]
         code, _ = pload(grp[0])
@@ -795,12 +815,12 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
             L.append("      " + pin(xs_ + gxs + ys_ + nxt_regs))
         L.append("    }")
         L.append(f"    float* __restrict__ gxo = gx + (size_t)n * {din};")
-        L += ["    " + ln for ln in vec_store(gxs, "gxo", f"{node_off[l]} + u * {d}")]
+        L += ["    " + ln for ln in vec_store(gxs, "gxo", f"{node_off[l]} + {UC} * {d}")]
         L.append("    break; }")
     L.append("  default: break;")
     L.append("  }")
     L.append("}")
-    info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups), nbgroups=len(bgroups),
+    info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups) * CG, nbgroups=len(bgroups) * CG,
                 npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, fwpb=TP_FWD_WPB, sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
@@ -1838,47 +1858,60 @@ def main(outdir: str) -> None:
              "template <typename V> __device__ __forceinline__ eelg_f2r eelg_pair(V v, int j) {",
              "  return (eelg_f2r){v[2 * j], v[2 * j + 1]};",
              "}", ""]
-    for lmax in kernel_sets.LMAX:
-        parts.append(emit_sh(lmax))
-    # the row a tp_fwd stream reads for an edge past its range (also when the batch has no
-    # edges and the edge tensors are empty): as long as the longest x / SH / weight row
-    pad = max(max(node.dim, (sh.dim + 3) // 4 * 4, sum(p.mul for p in cg.tp_paths(node, sh, target)))
-              for node, sh, target in tp_configs().values())
-    parts.append(f"__device__ __attribute__((aligned(16))) float eelg_tp_pad[{(pad + 3) // 4 * 4}];\n")
-    tp_table, sc_table = [], []
-    for name, (node, sh, target) in tp_configs().items():
-        code, info = emit_tp(name, node, sh, target)
-        parts.append(code)
-        parts.append(emit_tp(name, node, sh, target, "bf16")[0])
-        tp_table.append((name, info))
-    for name, (coupling, ls, corr) in sc_configs().items():
-        code, info = emit_sc(name, coupling, ls, corr)
-        parts.append(code)
-        sc_table.append((name, info))
-    # launch tables
-    parts.append("\n// ===== config tables =====")
-    parts.append("static const eelg_tp_cfg kTpConfigs[] = {")
-    for name, i in tp_table:
-        lmax = int(name.split("_l")[1])
-        parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
-                     f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                     f'tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw}},')
-    parts.append("};")
-    parts.append("static const eelg_sc_cfg kScConfigs[] = {")
-    for name, i in sc_table:
-        parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
-                     f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                     f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}, {i["cld"]}}},')
-    parts.append("};")
-    parts.append("const eelg_tp_cfg* eelg_tp_table(int* n) { *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }")
-    parts.append("const eelg_sc_cfg* eelg_sc_table(int* n) { *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }")
-    src = "\n".join(parts) + "\n"
-    path = os.path.join(outdir, "eelg_gen.hip")
-    old = open(path).read() if os.path.exists(path) else None
-    if old != src:
-        with open(path, "w") as f:
-            f.write(src)
-    print(f"wrote {path}: {len(src.splitlines())} lines")
+    header = parts
+    global MUL
+    for mul in kernel_sets.MULS:
+        MUL = mul
+        sfx = "" if mul == 32 else f"_m{mul}"
+        parts = list(header)
+        if mul == 32:
+            for lmax in kernel_sets.LMAX:
+                parts.append(emit_sh(lmax))
+        # the row a tp_fwd stream reads for an edge past its range (also when the batch has no
+        # edges and the edge tensors are empty): as long as the longest x / SH / weight row
+        pad = max(max(node.dim, (sh.dim + 3) // 4 * 4, sum(p.mul for p in cg.tp_paths(node, sh, target)))
+                  for node, sh, target in tp_configs().values())
+        parts.append(f"static __device__ __attribute__((aligned(16))) float eelg_tp_pad[{(pad + 3) // 4 * 4}];\n")
+        tp_table, sc_table = [], []
+        # bf16 storage of the edge tensors (BASELINE config 5) is generated for mul = 32 only
+        bf = mul == 32
+        for name, (node, sh, target) in tp_configs().items():
+            code, info = emit_tp(name + sfx, node, sh, target)
+            parts.append(code)
+            if bf:
+                parts.append(emit_tp(name + sfx, node, sh, target, "bf16")[0])
+            tp_table.append((name + sfx, info))
+        for name, (coupling, ls, corr) in sc_configs().items():
+            code, info = emit_sc(name + sfx, coupling, ls, corr)
+            parts.append(code)
+            sc_table.append((name + sfx, info))
+        # launch tables
+        parts.append("\n// ===== config tables =====")
+        parts.append(f"static const eelg_tp_cfg kTpConfigs[] = {{")
+        for name, i in tp_table:
+            lmax = int(name.split("_l")[1].split("_")[0])
+            bfk = (f"tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw" if bf
+                   else f"nullptr, nullptr, tp_bws_{name}, nullptr")
+            parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
+                         f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
+                         f'{bfk}}},')
+        parts.append("};")
+        parts.append("static const eelg_sc_cfg kScConfigs[] = {")
+        for name, i in sc_table:
+            parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
+                         f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
+                         f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}, {i["cld"]}}},')
+        parts.append("};")
+        parts.append(f"const eelg_tp_cfg* eelg_tp_table_m{mul}(int* n) {{ *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }}")
+        parts.append(f"const eelg_sc_cfg* eelg_sc_table_m{mul}(int* n) {{ *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }}")
+        src = "\n".join(parts) + "\n"
+        path = os.path.join(outdir, f"eelg_gen{sfx}.hip")
+        old = open(path).read() if os.path.exists(path) else None
+        if old != src:
+            with open(path, "w") as f:
+                f.write(src)
+        print(f"wrote {path}: {len(src.splitlines())} lines")
+    MUL = kernel_sets.MUL
 
 
 if __name__ == "__main__":

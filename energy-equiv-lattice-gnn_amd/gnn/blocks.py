@@ -222,6 +222,10 @@ class TensorProductInteractionBlock(torch.nn.Module):
                 "are built ('pna' is out of scope, SURVEY.md section 2)")
         # fail at construction, with the supported list, for structures without generated kernels
         kernel_sets.check_tp(self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
+        if storage_dtype != torch.float32 and kernel_sets.mul_of(self._node_feats_irreps) != kernel_sets.MUL:
+            raise NotImplementedError(
+                f"{storage_dtype} storage of the edge tensors is generated for {kernel_sets.MUL} "
+                f"channels only, not {self._node_feats_irreps}")
         self.linear_up = Linear(self._node_feats_irreps, self._node_feats_irreps)
         irreps_mid, instructions = cg.tp_out_irreps_with_instructions(
             self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)

@@ -6,17 +6,20 @@ the supported list, not at the first forward).
 Reference ``params`` space (``gnn/model.py:31-42``, ``gnn/mace.py:112-177``): ``lmax`` (SH),
 ``hidden_irreps``, ``correlation``.  Generated here:
 
-* tensor product: SH lmax 1..4, node irreps ``32x0e`` (first layer) or the natural-parity
-  hidden irreps ``32x0e+32x1o+...`` up to the SH lmax (later layers);
-* symmetric contraction: the same lmax, outputs = those hidden irreps, correlation 1..3.
-
-``mul`` (channels per irrep) is 32: one lane per channel in the interaction kernels.
+* tensor product: SH lmax 1..4, node irreps ``{mul}x0e`` (first layer) or the natural-parity
+  hidden irreps ``{mul}x0e+{mul}x1o+...`` up to the SH lmax (later layers);
+* symmetric contraction: the same lmax, outputs = those hidden irreps, correlation 1..3;
+* ``mul`` (channels per irrep) in ``MULS``: one lane per channel in the interaction kernels, a
+  half-wave per 32 channels (mul = 64: two channel groups; mul = 16: half a half-wave).  The
+  reference default and the benchmark configurations are 32; bf16 storage of the edge tensors
+  (BASELINE config 5) is generated for 32 only.
 """
 from __future__ import annotations
 
 from typing import Tuple
 
 MUL = 32
+MULS = (16, 32, 64)
 LMAX = (1, 2, 3, 4)
 CORRELATIONS = (1, 2, 3)
 
@@ -35,17 +38,24 @@ def coupling_str(lmax: int) -> str:
 
 def supported_text() -> str:
     return (f"generated kernel sets: SH lmax in {LMAX} with hidden_irreps "
-            f"'{hidden_irreps_str(1)}' .. '{hidden_irreps_str(4)}' (32 channels of every l up to "
-            f"the SH lmax), correlation in {CORRELATIONS}")
+            f"'{hidden_irreps_str(1)}' .. '{hidden_irreps_str(4)}' (mul channels of every l up to "
+            f"the SH lmax, mul in {MULS}), correlation in {CORRELATIONS}")
+
+
+def mul_of(irreps) -> int:
+    """the channel count of an all-equal-mul irreps (0 when the muls differ)"""
+    muls = {m for m, _ in irreps}
+    return muls.pop() if len(muls) == 1 else 0
 
 
 def check_tp(node, sh, target) -> None:
     """Raise NotImplementedError unless the interaction (node irreps x SH -> target) is a
     generated tensor-product set."""
     lmax = sh.lmax
-    ok = (lmax in LMAX and str(sh) == str(_sh(lmax))
-          and str(node) in (f"{MUL}x0e", hidden_irreps_str(lmax))
-          and str(target) == coupling_target(lmax))
+    mul = mul_of(node)
+    ok = (lmax in LMAX and mul in MULS and str(sh) == str(_sh(lmax))
+          and str(node) in (f"{mul}x0e", hidden_irreps_str(lmax, mul))
+          and str(target) == coupling_target(lmax, mul))
     if not ok:
         raise NotImplementedError(
             f"no HIP tensor-product kernels for {node} x {sh} -> {target}; {supported_text()}")
@@ -54,7 +64,8 @@ def check_tp(node, sh, target) -> None:
 def check_sc(irreps_in, ls: Tuple[int, ...], correlation: int) -> None:
     """Raise NotImplementedError unless the symmetric contraction is a generated set."""
     lmax = irreps_in.lmax
-    ok = (lmax in LMAX and str(irreps_in) == hidden_irreps_str(lmax)
+    mul = mul_of(irreps_in)
+    ok = (lmax in LMAX and mul in MULS and str(irreps_in) == hidden_irreps_str(lmax, mul)
           and tuple(ls) == tuple(range(lmax + 1)) and correlation in CORRELATIONS)
     if not ok:
         raise NotImplementedError(
@@ -62,9 +73,9 @@ def check_sc(irreps_in, ls: Tuple[int, ...], correlation: int) -> None:
             f"correlation {correlation}; {supported_text()}")
 
 
-def coupling_target(lmax: int) -> str:
+def coupling_target(lmax: int, mul: int = MUL) -> str:
     """The interaction irreps ``(SH * mul).sort().simplify()`` (``gnn/model.py:36-37``)."""
-    return hidden_irreps_str(lmax)
+    return hidden_irreps_str(lmax, mul)
 
 
 def _sh(lmax: int):

@@ -419,9 +419,10 @@ class _SymCon(torch.autograd.Function):
     def forward(ctx, x, coef, cfg: int, info: Dict[str, int], mul: int, side=None):
         x, coef = _a16(x), _a16(coef)
         n = x.shape[0]
-        if x.shape[1] != info["x_row"] or coef.shape != (mul, info["coef_ld"]):
-            raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs {info}")
-        out = torch.empty(n, info["out_row"], device=x.device, dtype=torch.float32)
+        # rows of mul channels x D (Dout) components; info's x_row / out_row are those of mul 32
+        if x.shape[1] != mul * info["D"] or coef.shape != (mul, info["coef_ld"]):
+            raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs mul {mul}, {info}")
+        out = torch.empty(n, mul * info["Dout"], device=x.device, dtype=torch.float32)
         lib = _lib.load()
         tok = TIMER.start("sc_fwd")
         _lib.check(lib.eelg_sc_fwd(cfg, _lib.ptr(x), _lib.ptr(coef), n, mul, _lib.ptr(out),

@@ -170,13 +170,13 @@ int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, 
  * with the linear split by input block: ps = x W_s^T, pr = x W_r^T + b ([N, 2D], values
  * then multipliers), ep = edge_ft W_e^T ([E, 2D], receiver-sorted edge order).
  * agg[n] = row_scale[n] * sum_e softplus(zv) sigmoid(zm)  (row_scale NULL -> 'sum').
- * Built for D <= 128 (the benchmark models use 128 and 64); -2 otherwise. */
+ * Built for D <= EELG_CGC_MAXD (the benchmark models use 128 and 64); -2 otherwise. */
 #define EELG_CGC_MAXD 256   /* node_dim of the built CGC kernels (one lane per 64 channels, <= 4) */
 int eelg_cgc_fwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D, float* agg,
                  void* stream);
 /* Backward: dz[E, 2D] = d agg / d z per edge and grad_pr[N, 2D] = receiver sums of dz;
- * the sender sums are eelg_segment_sum_csr(dz, srowptr, sperm).  D <= 128 as the forward. */
+ * the sender sums are eelg_segment_sum_csr(dz, srowptr, sperm).  D <= EELG_CGC_MAXD as the forward. */
 int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* sender,
                  const int* rowptr, const float* row_scale, int n_nodes, int D,
                  const float* grad_agg, float* dz, float* grad_pr, void* stream);

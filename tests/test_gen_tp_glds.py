@@ -4,9 +4,10 @@ The kernel moves one half-wave's rows for one edge as a static list of 16-byte c
 chunks per ``global_load_lds_dwordx4`` wave-instruction, and reads its operands back from the
 lane-linear image at the float offsets the generator recorded.  For every generated TP set this
 checks that the chunk list:
-* covers, exactly once and in order, the group's 32-float weight slices (first when
+* covers, exactly once and in order, the group's weight slices of its channel group (first when
   ``TP_FWD_WNT``: the weight-only LDS-DMA instructions then carry the nontemporal policy), the
-  x blocks of the group's l1 values and the whole padded SH row;
+  x blocks of the group's l1 values (the channel group's part of each) and the whole padded SH
+  row, for mul 16 / 32 / 64 (channel groups: mul = 64 two groups of 32, mul = 16 one of 16);
 * has every source piece 16-byte aligned and inside its row (x: din, SH: the padded nshp,
   w: wn floats), so no LDS-DMA load leaves the tensors it reads;
 * fits the image the kernel declares (ceil(chunks / 64) instructions of 64 chunks) and the
@@ -27,10 +28,15 @@ import gen_kernels as gk  # noqa: E402
 from gnn import cg  # noqa: E402
 
 CONFIGS = gk.tp_configs()
+MULS = gk.kernel_sets.MULS
 
 
-def _setup(name):
-    node, sh, target = CONFIGS[name]
+def _setup(name, mul=32):
+    saved, gk.MUL = gk.MUL, mul
+    try:
+        node, sh, target = gk.tp_configs()[name]
+    finally:
+        gk.MUL = saved
     paths = cg.tp_paths(node, sh, target)
     groups = gk._group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), gk.TP_MAXACC)
     node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
@@ -39,33 +45,51 @@ def _setup(name):
     return node, groups, node_off, nshp, wn
 
 
-@pytest.mark.parametrize("name", sorted(CONFIGS))
-def test_chunk_lists_cover_the_rows_once_and_stay_in_bounds(name):
-    node, groups, node_off, nshp, wn = _setup(name)
-    din = node.dim
-    for (need_l1, need_l2, chunks, fo_x, fo_sh, fo_w), grp in zip(
-            gk._glds_chunks(groups, nshp, node_off), groups):
-        assert need_l1 == sorted({p.l1 for p in grp})
-        expect = []
+def _chunks(groups, nshp, node_off, mul, c):
+    saved, gk.MUL = gk.MUL, mul
+    try:
+        return gk._glds_chunks(groups, nshp, node_off, 4, c)
+    finally:
+        gk.MUL = saved
 
-        def weights():
-            for p in grp:
-                assert fo_w[p.slot] == 4 * len(expect)
-                expect.extend((2, 4 * gk.MUL * p.slot + 16 * c) for c in range(8))
-        if gk.TP_FWD_WNT:
-            weights()
-        for l in need_l1:
-            assert fo_x[l] == 4 * len(expect)
-            expect += [(0, 4 * node_off[l] + 16 * c) for c in range(8 * (2 * l + 1))]
-        assert fo_sh == 4 * len(expect)
-        expect += [(1, 16 * c) for c in range(nshp // 4)]
-        if not gk.TP_FWD_WNT:
-            weights()
-        assert chunks == expect
-        row_bytes = {0: 4 * din, 1: 4 * nshp, 2: 4 * wn}
-        for kind, off in chunks:
-            assert off % 16 == 0 and 0 <= off and off + 16 <= row_bytes[kind]
-        assert len(set(chunks)) == len(chunks)
+
+@pytest.mark.parametrize("mul", MULS)
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_chunk_lists_cover_the_rows_once_and_stay_in_bounds(name, mul):
+    node, groups, node_off, nshp, wn = _setup(name, mul)
+    din = node.dim
+    n_cg, lw = max(1, mul // 32), min(mul, 32)
+    seen = {0: set(), 2: set()}
+    for c in range(n_cg):
+        for (need_l1, need_l2, chunks, fo_x, fo_sh, fo_w), grp in zip(
+                _chunks(groups, nshp, node_off, mul, c), groups):
+            assert need_l1 == sorted({p.l1 for p in grp})
+            expect = []
+
+            def weights():
+                for p in grp:
+                    assert fo_w[p.slot] == 4 * len(expect)
+                    expect.extend((2, 4 * (mul * p.slot + c * lw) + 16 * k) for k in range(lw // 4))
+            if gk.TP_FWD_WNT:
+                weights()
+            for l in need_l1:
+                assert fo_x[l] == 4 * len(expect)
+                expect += [(0, 4 * (node_off[l] + c * lw * (2 * l + 1)) + 16 * k)
+                           for k in range(lw * (2 * l + 1) // 4)]
+            assert fo_sh == 4 * len(expect)
+            expect += [(1, 16 * k) for k in range(nshp // 4)]
+            if not gk.TP_FWD_WNT:
+                weights()
+            assert chunks == expect
+            row_bytes = {0: 4 * din, 1: 4 * nshp, 2: 4 * wn}
+            for kind, off in chunks:
+                assert off % 16 == 0 and 0 <= off and off + 16 <= row_bytes[kind]
+                if kind != 1:
+                    seen[kind].add(off)
+            assert len(set(chunks)) == len(chunks)
+    # over all path groups and channel groups, every x block and weight slice is moved once
+    assert len(seen[2]) == wn // 4
+    assert len(seen[0]) == sum(mul * ir.dim for _, ir in node) // 4
 
 
 def _eval_desc(line, lane):

@@ -36,9 +36,10 @@ def test_tp_interaction_bf16_storage(lmax, layer0):
     bd = b.to(DEV)
     csr = ops.EdgeCSR.build(bd.edge_index, b.node_attrs.shape[0])
     sh_ir = Irreps.spherical_harmonics(lmax)
-    node = Irreps("32x0e") if layer0 else Irreps(
-        "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
-    target = (sh_ir * 32).sort()[0].simplify()
+    mul = 32
+    node = Irreps(f"{mul}x0e") if layer0 else Irreps(
+        "+".join(f"{mul}x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+    target = (sh_ir * mul).sort()[0].simplify()
     idx, info = _lib.tp_config_by_sig(cg.fnv1a64(cg.tp_signature(node, sh_ir, target)))
     sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[csr.perm],
                            bd.edge_attr[csr.perm].reshape(-1), lmax, 6, 0.6, rmax)
@@ -119,9 +120,10 @@ def test_model_bf16_storage_matches_oracle(lmax):
                   grad_all=rel_err(gm, go), cos_min=cos_min)
 
 
-@pytest.mark.parametrize("lmax,layer0,bf", [(4, False, False), (4, True, False), (3, False, False),
-                                            (4, False, True), (3, False, True)])
-def test_tp_bwd_sender_order_matches_edge_order(lmax, layer0, bf):
+@pytest.mark.parametrize("lmax,layer0,bf,mul", [(4, False, False, 32), (4, True, False, 32), (3, False, False, 32),
+                                                (4, False, True, 32), (3, False, True, 32),
+                                                (4, False, False, 16), (4, False, False, 64), (2, True, False, 64)])
+def test_tp_bwd_sender_order_matches_edge_order(lmax, layer0, bf, mul):
     """eelg_tp_bwd_sender (grad_x summed per sender in registers) vs eelg_tp_bwd + the sender
     segment sum, on a graph whose first 7 nodes send nothing (their grad_x must be 0).
     grad_w: the same per-edge expression (fma contraction may differ) -> 1e-6 fp32, one
@@ -135,9 +137,9 @@ def test_tp_bwd_sender_order_matches_edge_order(lmax, layer0, bf):
     bd = b.to(DEV)
     csr = ops.EdgeCSR.build(ei.to(DEV), b.node_attrs.shape[0])
     sh_ir = Irreps.spherical_harmonics(lmax)
-    node = Irreps("32x0e") if layer0 else Irreps(
-        "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
-    target = (sh_ir * 32).sort()[0].simplify()
+    node = Irreps(f"{mul}x0e") if layer0 else Irreps(
+        "+".join(f"{mul}x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1)))
+    target = (sh_ir * mul).sort()[0].simplify()
     idx, info = _lib.tp_config_by_sig(cg.fnv1a64(cg.tp_signature(node, sh_ir, target)))
     sh, _ = ops.edge_embed(bd.positions, csr, bd.shifts[keep.to(DEV)][csr.perm],
                            bd.edge_attr[keep.to(DEV)][csr.perm].reshape(-1), lmax, 6, 0.6, rmax)

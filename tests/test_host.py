@@ -135,23 +135,29 @@ def test_library_loads_and_exports_every_header_symbol():
 
 def test_library_config_tables_match_host_structure():
     """Every kernel set gnn/kernel_sets.py lists is in the library under its name, with the
-    structure hash the host derives (lmax 1..4, correlation 1..3)."""
+    structure hash the host derives (lmax 1..4, correlation 1..3, mul 16 / 32 / 64: mul 32 under
+    the plain names, the others with an _m<mul> suffix)."""
     from gnn import _lib, kernel_sets
+    for mul in kernel_sets.MULS:
+        sfx = "" if mul == 32 else f"_m{mul}"
+        for lmax in kernel_sets.LMAX:
+            sh = Irreps.spherical_harmonics(lmax)
+            target = (sh * mul).sort()[0].simplify()
+            hid = Irreps(kernel_sets.hidden_irreps_str(lmax, mul))
+            for name, node in ((f"tpA_l{lmax}{sfx}", Irreps(f"{mul}x0e")), (f"tpB_l{lmax}{sfx}", hid)):
+                _, info, sig = _lib.tp_config(name)
+                paths = cg.tp_paths(node, sh, target)
+                assert info["din"] == node.dim and info["npaths"] == len(paths)
+                assert info["wn"] == mul * len(paths) and info["nsh"] == sh.dim
+                assert sig == cg.fnv1a64(cg.tp_signature(node, sh, target))
+                assert _lib.tp_config_by_sig(sig)[0] == _lib.tp_config(name)[0]
     for lmax in kernel_sets.LMAX:
-        sh = Irreps.spherical_harmonics(lmax)
-        target = (sh * 32).sort()[0].simplify()
-        hid = Irreps(kernel_sets.hidden_irreps_str(lmax))
-        for name, node in ((f"tpA_l{lmax}", Irreps("32x0e")), (f"tpB_l{lmax}", hid)):
-            _, info, sig = _lib.tp_config(name)
-            paths = cg.tp_paths(node, sh, target)
-            assert info["din"] == node.dim and info["npaths"] == len(paths)
-            assert info["wn"] == 32 * len(paths) and info["nsh"] == sh.dim
-            assert sig == cg.fnv1a64(cg.tp_signature(node, sh, target))
         coupling = kernel_sets.coupling_str(lmax)
         for corr in kernel_sets.CORRELATIONS:
             _, info, sig = _lib.sc_config(f"sc_l{lmax}_c{corr}")
             plan = cg.symcon_plan(coupling, tuple(range(lmax + 1)), corr)
             assert info["nterms"] == len(plan.terms) and info["x_row"] == 32 * plan.D
+            assert info["D"] == plan.D
             assert sig == cg.fnv1a64(cg.sc_signature(coupling, tuple(range(lmax + 1)), corr))
     with pytest.raises(_lib.EELGError):
         _lib.tp_config("no_such_config")
@@ -164,19 +170,26 @@ def test_unsupported_params_fail_at_construction_with_the_supported_list():
     from helpers import params
     from gnn.model import EnergyEquivGNN
     for change in (dict(lmax=5, hidden_irreps="32x0e+32x1o+32x2e+32x3o+32x4e+32x5o"),
-                   dict(hidden_irreps="64x0e+64x1o+64x2e+64x3o+64x4e"),
+                   dict(hidden_irreps="48x0e+48x1o+48x2e+48x3o+48x4e"),
+                   dict(hidden_irreps="32x0e+16x1o+32x2e+32x3o+32x4e"),
                    dict(hidden_irreps="32x0e+32x1o+32x2e"),
                    dict(correlation=4)):
         p = Namespace(**{**vars(params(2)), **change})
         with pytest.raises(NotImplementedError, match="generated kernel sets"):
             EnergyEquivGNN(p)
+    from gnn import kernel_sets
     for lmax in (1, 2, 3, 4):
         for corr in (1, 2, 3):
-            from gnn import kernel_sets
-            p = Namespace(**{**vars(params(2)), "lmax": lmax, "correlation": corr,
-                             "hidden_irreps": kernel_sets.hidden_irreps_str(lmax),
-                             "readout_irreps": kernel_sets.hidden_irreps_str(lmax, 16)})
-            EnergyEquivGNN(p)
+            for mul in kernel_sets.MULS:
+                p = Namespace(**{**vars(params(2)), "lmax": lmax, "correlation": corr,
+                                 "hidden_irreps": kernel_sets.hidden_irreps_str(lmax, mul),
+                                 "readout_irreps": kernel_sets.hidden_irreps_str(lmax, 16)})
+                EnergyEquivGNN(p)
+    # bf16 storage of the edge tensors is generated for 32 channels only
+    p = Namespace(**{**vars(params(2)), "hidden_irreps": kernel_sets.hidden_irreps_str(4, 64),
+                     "storage_dtype": "bfloat16"})
+    with pytest.raises(NotImplementedError, match="storage"):
+        EnergyEquivGNN(p)
 
 
 def test_product_rejects_cpu_tensors_loudly():
