@@ -35,6 +35,9 @@ from gnn.irreps import Ir, Irreps  # noqa: E402
 MUL = kernel_sets.MUL
 # receivers per half-wave in tp_fwd (the launcher reads it from the config table)
 TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
+# measurement variant (never the product): tp_fwd computes every aggregate but stores none, the
+# lower bound of a forward that hands agg to a fused epilogue instead of HBM
+TP_FWD_NOSTORE = int(os.environ.get("EELG_TP_FWD_NOSTORE", "0"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
 # tp_fwd waves per workgroup (a node tile = 2 x TP_FWD_WPB x TP_NPH receivers; one-wave
 # workgroups refill a freed wave slot at once: r03z kbench 0.505 vs 0.520 ms at 4, 0.518 at 2;
@@ -535,7 +538,8 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
         L.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the image is refilled')
         for h in (0, 1):
             L.append(f"      while (node_{h} < n1_{h} && nend_{h} == e_{h}) {{   // uniform")
-            L.append(f"        if (hf == {h}{f' && u < {LW}' if LW < 32 else ''}) {{")
+            nost = " && inv_norm < -1.0e30f" if TP_FWD_NOSTORE else ""   # measurement variant only
+            L.append(f"        if (hf == {h}{f' && u < {LW}' if LW < 32 else ''}{nost}) {{")
             L.append(f"          float* __restrict__ o = agg + (size_t)node_{h} * {dmid};")
             for p in grp:
                 d3 = 2 * p.l3 + 1

@@ -10,5 +10,5 @@ cp -r "$R/energy-equiv-lattice-gnn_amd/csrc" "$T/a/p/csrc"
 cp -r "$R/energy-equiv-lattice-gnn_amd/gnn" "$T/a/p/gnn"
 cp -r "$R/include" "$T/a/include"
 rm -rf "$T/a/p/csrc/build" "$T/a/p/csrc/generated"
-make -s -C "$T/a/p/csrc" OUT="$R/variants/libeelg_$1.so" > "$T/build.log" 2>&1 || { tail -20 "$T/build.log"; exit 1; }
+make -s -j4 -C "$T/a/p/csrc" OUT="$R/variants/libeelg_$1.so" > "$T/build.log" 2>&1 || { tail -20 "$T/build.log"; exit 1; }
 echo "built variants/libeelg_$1.so"
