@@ -2,9 +2,7 @@
 """Disassembly of kernels in gnn/libeelg.so (no GPU needed): the instruction histogram of every
 kernel whose name matches a regex, or its full listing.
 
-  python tools/kernel_isa.py <regex> [--list] [--top N] [--meta]
-
---meta prints the code-object metadata instead (VGPRs, AGPRs, SGPRs, spills, LDS bytes, scratch).
+  python tools/kernel_isa.py <regex> [--list] [--top N]
 """
 import argparse
 import collections
@@ -39,23 +37,11 @@ def main():
     ap.add_argument("regex")
     ap.add_argument("--list", action="store_true")
     ap.add_argument("--top", type=int, default=15)
-    ap.add_argument("--meta", action="store_true")
     a = ap.parse_args()
     so = os.environ.get("EELG_LIB") or os.path.join(ROOT, "energy-equiv-lattice-gnn_amd", "gnn", "libeelg.so")
     pat = re.compile(a.regex)
     with tempfile.TemporaryDirectory() as d:
         for co in code_objects(so, d):
-            if a.meta:
-                notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True,
-                                       text=True).stdout
-                for blk in notes.split("  - .agpr_count:")[1:]:
-                    f = dict(re.findall(r"\.(\w+):\s+(\S+)", blk))
-                    if pat.search(f.get("name", "")):
-                        print(f"{f['name']}: vgpr {f.get('vgpr_count')} agpr {blk.split()[0]} sgpr "
-                              f"{f.get('sgpr_count')} spills v{f.get('vgpr_spill_count')}/s"
-                              f"{f.get('sgpr_spill_count')} lds {f.get('group_segment_fixed_size')} "
-                              f"scratch {f.get('private_segment_fixed_size')}")
-                continue
             dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co],
                                  capture_output=True, text=True).stdout
             cur, body = None, []
