@@ -13,6 +13,7 @@ address a column block of a wider weight (the sender / receiver / edge blocks of
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -21,6 +22,15 @@ from . import _lib, ops
 
 LINW_WG = 4096          # weight-gradient workgroups (node slices x 32x32 tiles), as o3.Linear
 LINW_MAX_SLICES = 128
+# forward / grad-x with K in [LIN_X6_MINK, 320] (whole 32-wide chunks, n_out % 32 == 0) on the
+# fp32-accurate split-bf16 packed kernel (eelg_linear_fwd_pk), the weight packed per call
+# (~7 us; the CGC layer's [W_v; W_m] is a fresh concatenation every forward, so a cache keyed
+# by address and version could hand back a stale pack).  The CGC projections (K = 128 / 256 at
+# 262k rows) run at ~144 TFLOP/s on the fp32 MFMA, its peak; the split form does a 16-deep K
+# block in 3/8 of the MFMA cycles.  r05v, 150-step runs alternating on one box: 30,001 / 30,513
+# / 30,907 vs 29,003 / 29,356 / 29,393 graphs/s (fp32); traced linear time 3.29 vs 3.73 ms/step
+# (r05s).  EELG_DENSE_X6=0: the fp32 kernels.
+DENSE_X6 = os.environ.get("EELG_DENSE_X6", "1") != "0"
 
 
 def _slot_desc(n_out: int, k: int, w_off: int, ldk: int, ldj: int, bias: bool, n: int):
@@ -37,6 +47,23 @@ def _slot_desc(n_out: int, k: int, w_off: int, ldk: int, ldj: int, bias: bool, n
     return d
 
 
+def _x6(x, w, bias, res, n, y, n_out, k, desc) -> bool:
+    from .o3 import LIN_X6_MINK
+    if not (DENSE_X6 and k % 32 == 0 and LIN_X6_MINK <= k <= 320 and n_out % 32 == 0
+            and x.shape[1] % 4 == 0 and x.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
+            and (res is None or res.data_ptr() % 16 == 0)):
+        return False
+    lib = _lib.load()
+    pk = torch.empty(3, int(lib.eelg_linear_pack_size(ctypes.byref(desc))), device=w.device,
+                     dtype=torch.bfloat16)
+    _lib.check(lib.eelg_linear_pack(_lib.ptr(w), ctypes.byref(desc), _lib.ptr(pk), _lib.stream(pk)),
+               "dense_pack")
+    _lib.check(lib.eelg_linear_fwd_pk(
+        _lib.ptr(x), x.shape[1], _lib.ptr(pk), _lib.ptr(bias), _lib.ptr(res), n, _lib.ptr(y), n_out,
+        ctypes.byref(desc), _lib.stream(y)), "dense_fwd_pk")
+    return True
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, n_out: int, k: int, w_off: int = 0,
                ld: Optional[int] = None, bias: Optional[torch.Tensor] = None,
                res: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -46,6 +73,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, n_out: int, k: int, w_off: int 
     n = x.shape[0]
     y = torch.empty(n, n_out, device=x.device, dtype=torch.float32)
     desc = _slot_desc(n_out, k, w_off, 1, ld, bias is not None, n)
+    if _x6(x, w, bias, res, n, y, n_out, k, desc):
+        return y
     _lib.check(_lib.load().eelg_linear_fwd_res(
         _lib.ptr(x), x.shape[1], _lib.ptr(w), _lib.ptr(bias), _lib.ptr(res), n, _lib.ptr(y), n_out,
         ctypes.byref(desc), _lib.stream(y)), "dense_fwd")
@@ -59,6 +88,8 @@ def linear_bwd_x(gy: torch.Tensor, w: torch.Tensor, n_out: int, k: int, w_off: i
     n = gy.shape[0]
     gx = torch.empty(n, k, device=gy.device, dtype=torch.float32)
     desc = _slot_desc(k, n_out, w_off, ld, 1, False, n)
+    if _x6(gy, w, None, res, n, gx, k, n_out, desc):
+        return gx
     _lib.check(_lib.load().eelg_linear_fwd_res(
         _lib.ptr(gy), gy.shape[1], _lib.ptr(w), None, _lib.ptr(res), n, _lib.ptr(gx), k,
         ctypes.byref(desc), _lib.stream(gx)), "dense_bwd_x")

@@ -17,25 +17,41 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"])
     args = ap.parse_args()
     import bench
     from gnn import EnergyEquivGNN
     from gnn.data import collate
     from gnn.synthetic import SyntheticLattices
     from gnn.train import stiffness_loss
-    ds = SyntheticLattices(32, 1024, 4096, 1234)
-    mine = [ds[g] for g in range(32)]
-    params = bench.make_params(4, max(float(d.edge_attr.max()) for d in mine))
-    torch.manual_seed(0)
-    model = EnergyEquivGNN(params).cuda()
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True, fused=True)
-    batch = collate(mine).to("cuda")
-    model.edge_graph(batch)
+    if args.model == "egnn":
+        ds = SyntheticLattices(32, 1024, 4096, 1234)
+        mine = [ds[g] for g in range(32)]
+        params = bench.make_params(4, max(float(d.edge_attr.max()) for d in mine))
+        torch.manual_seed(0)
+        model = EnergyEquivGNN(params).cuda()
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True, fused=True)
+        batch = collate(mine).to("cuda")
+        target = batch.stiffness
+    else:   # bench.main_cgc's model, batch and optimizer (256 graphs)
+        from argparse import Namespace
+        from gnn import cgc
+        modified = args.model == "cgc_modified"
+        p = Namespace(hidden_irreps=128 if modified else 64, interaction_reduction="sum",
+                      global_reduction="mean", message_passes=3, positive="square")
+        ds = SyntheticLattices(256, 1024, 4096, 1234)
+        batch = collate([ds[g] for g in range(256)]).to("cuda")
+        torch.manual_seed(0)
+        model = (cgc.CrystGraphConv if modified else cgc.CrystGraphConvVanilla)(p).cuda()
+        iu = torch.triu_indices(6, 6)
+        target = batch.stiffness if modified else batch.stiffness[:, iu[0], iu[1]]
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, amsgrad=True, weight_decay=1e-8)
+    EnergyEquivGNN.edge_graph(batch)
     plist = list(model.parameters())
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss = stiffness_loss(model(batch)["stiffness"], batch.stiffness)
+        loss = stiffness_loss(model(batch)["stiffness"], target)
         loss.backward()
         torch.nn.utils.clip_grad_norm_(plist, 10.0)
         opt.step()
@@ -46,7 +62,7 @@ def main():
     def step_parts():
         t0 = time.perf_counter()
         opt.zero_grad(set_to_none=True)
-        loss = stiffness_loss(model(batch)["stiffness"], batch.stiffness)
+        loss = stiffness_loss(model(batch)["stiffness"], target)
         t1 = time.perf_counter()
         loss.backward()
         t2 = time.perf_counter()
