@@ -1045,4 +1045,24 @@ int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int 
   return check_launch("linear_bwd_w");
 }
 
+int eelg_linear_bwd_w_x6(const float* g, int ldg, const float* x, int ldx, int n_rows, int n_out,
+                         int k, int tiles_per_split, float* partial, void* stream) {
+  if (k != 32 && k != 64 && k != 96 && k != 128)
+    return fail(-2, "linear_bwd_w_x6: k must be 32, 64, 96 or 128, got %d", k);
+  if (n_out <= 0 || tiles_per_split <= 0 || ldg < n_out || ldx < k)
+    return fail(-2, "linear_bwd_w_x6: bad shape (n_out %d, ldg %d, k %d, ldx %d, tiles %d)", n_out,
+                ldg, k, ldx, tiles_per_split);
+  if (n_rows <= 0) return 0;
+  const int ntile = (n_rows + 31) / 32;
+  const dim3 grid((n_out + 127) / 128, (ntile + tiles_per_split - 1) / tiles_per_split);
+  hipStream_t st = (hipStream_t)stream;
+  switch (k / 32) {
+    case 1: hipLaunchKernelGGL(lin_bwdw_x6_kernel<1>, grid, dim3(256), 0, st, g, ldg, x, ldx, n_rows, n_out, tiles_per_split, partial); break;
+    case 2: hipLaunchKernelGGL(lin_bwdw_x6_kernel<2>, grid, dim3(256), 0, st, g, ldg, x, ldx, n_rows, n_out, tiles_per_split, partial); break;
+    case 3: hipLaunchKernelGGL(lin_bwdw_x6_kernel<3>, grid, dim3(256), 0, st, g, ldg, x, ldx, n_rows, n_out, tiles_per_split, partial); break;
+    default: hipLaunchKernelGGL(lin_bwdw_x6_kernel<4>, grid, dim3(256), 0, st, g, ldg, x, ldx, n_rows, n_out, tiles_per_split, partial); break;
+  }
+  return check_launch("linear_bwd_w_x6");
+}
+
 }  // extern "C"

@@ -1014,3 +1014,94 @@ __global__ __launch_bounds__(256) void lin_pack_kernel(const float* __restrict__
 #pragma unroll
   for (int q = 0; q < 3; ++q) pk[o + q * 64] = p[q];
 }
+
+// ---------------------------------------------------------------------------------------------
+// Dense weight gradient on bf16 MFMA with fp32-accurate split operands (round 5):
+//   part[s, j, k] = sum over split s's rows r of g[r, j] * x[r, k]
+// = the torch-layout grad W = g^T x of a Linear y = x W^T (summed over s by eelg_sum_rows).
+// Both operands are data and are split per element on the fly (eelg_split8).  A wave owns 32
+// output rows j: A[j][r] = g[r][j], 16 values per lane per 32-row tile, coalesced over j.  The
+// tile's x rows [32 x 32 NT] are split once per workgroup into LDS in B-fragment order, shared
+// by the 4 waves and double buffered (the barrier of tile t separates tile t-2's reads of a
+// buffer from its rewrite).  K = rows, two K = 16 blocks per tile; hi / lo accumulators
+// (EELG_X6HL).  For the CGC projections (n_out 256, k 128, 262k rows) the fp32 grad-W kernel
+// runs at the fp32 MFMA peak; this form does a K = 16 block in 3/8 of its MFMA cycles.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void lin_bwdw_x6_kernel(const float* __restrict__ g, int ldg,
+                                                          const float* __restrict__ x, int ldx,
+                                                          int n_rows, int n_out,
+                                                          int tiles_per_split,
+                                                          float* __restrict__ part) {
+  constexpr int NFR = NT * 2 * 64;              // B fragments per part: ((ct, kb), hf, column)
+  constexpr int FPT = (NFR + 255) / 256;        // fragments each thread builds
+  constexpr int K = NT * 32;
+  __shared__ uint4 xs[2][3 * NFR];
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, i = l & 31, hf = l >> 5;
+  const int j = blockIdx.x * 128 + wave * 32 + i;
+  const int s = blockIdx.y;
+  const int ntile = (n_rows + 31) >> 5;
+  const int t0 = s * tiles_per_split, t1 = min(ntile, t0 + tiles_per_split);
+  eelg_f32x16v acc[NT], lo[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ct][r] = lo[ct][r] = 0.0f;
+  float an[16], xn[FPT][8];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = t * 32 + 16 * kb + 8 * hf + u;
+        an[8 * kb + u] = (r < n_rows && j < n_out) ? g[(size_t)r * ldg + j] : 0.0f;
+      }
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fi = threadIdx.x + 256 * f;
+      const int bk = fi & 31, bh = (fi >> 5) & 1, bkb = (fi >> 6) & 1, bct = fi >> 7;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = t * 32 + 16 * bkb + 8 * bh + u;
+        xn[f][u] = (fi < NFR && r < n_rows) ? x[(size_t)r * ldx + bct * 32 + bk] : 0.0f;
+      }
+    }
+  };
+  if (t0 < t1) load(t0);
+  for (int t = t0; t < t1; ++t) {
+    uint4* __restrict__ hb = xs[t & 1];
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fi = threadIdx.x + 256 * f;
+      if (fi < NFR) {
+        uint4 pp[3];
+        eelg_split8(xn[f], pp);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) hb[p * NFR + fi] = pp[p];
+      }
+    }
+    __syncthreads();
+    uint4 ap[2][3];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) eelg_split8(&an[8 * kb], ap[kb]);
+    if (t + 1 < t1) load(t + 1);   // in flight during the MFMAs
+    const uint4* __restrict__ bb = hb + hf * 32 + i;
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        uint4 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = bb[p * NFR + (ct * 2 + kb) * 64];
+        EELG_X6HL(acc[ct], lo[ct], ap[kb], b);
+      }
+  }
+  const int jb = blockIdx.x * 128 + wave * 32;
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = jb + (r & 3) + 8 * (r >> 2) + 4 * hf;
+      if (jj < n_out) part[((size_t)s * n_out + jj) * K + ct * 32 + i] = acc[ct][r] + lo[ct][r];
+    }
+}

@@ -57,6 +57,7 @@ _SIGS = {
     "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_fwd_res": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
+    "eelg_linear_bwd_w_x6": ([_P, _I, _P, _I, _I, _I, _I, _I, _P, _P], _I),
     "eelg_radial_plan": ([_I, _I, _P, _P], _I),
     "eelg_linear_pack_size": ([_P], ctypes.c_longlong),
     "eelg_linear_pack": ([_P, _P, _P, _P], _I),

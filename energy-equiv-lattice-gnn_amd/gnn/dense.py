@@ -31,6 +31,11 @@ LINW_MAX_SLICES = 128
 # / 30,907 vs 29,003 / 29,356 / 29,393 graphs/s (fp32); traced linear time 3.29 vs 3.73 ms/step
 # (r05s).  EELG_DENSE_X6=0: the fp32 kernels.
 DENSE_X6 = os.environ.get("EELG_DENSE_X6", "1") != "0"
+# the weight gradient on the same split form when K (= the Linear's input width) is 32..128
+# and there are enough rows for the MFMA tiles to pay: workgroups of 128 output rows x a split
+# of rows (eelg_linear_bwd_w_x6)
+LINW_X6_MINROWS = 4096
+LINW_X6_WG = int(os.environ.get("EELG_LINW_X6_WG", "512"))
 
 
 def _slot_desc(n_out: int, k: int, w_off: int, ldk: int, ldj: int, bias: bool, n: int):
@@ -104,6 +109,18 @@ def linear_bwd_w(x: torch.Tensor, gy: torch.Tensor) -> torch.Tensor:
     n_out = gy.shape[1]
     if n == 0:
         return torch.zeros(n_out, k, device=x.device, dtype=torch.float32)
+    if DENSE_X6 and k in (32, 64, 96, 128) and n >= LINW_X6_MINROWS:
+        # split-bf16 MFMA (eelg_linear_bwd_w_x6): about LINW_X6_WG workgroups of 128 output rows
+        # x one row split each, partials [splits, n_out, k] summed in a fixed order
+        ntile = -(-n // 32)
+        nblk = -(-n_out // 128)
+        tps = max(1, -(-ntile // max(1, LINW_X6_WG // nblk)))
+        splits = -(-ntile // tps)
+        part = torch.empty(splits, n_out * k, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().eelg_linear_bwd_w_x6(
+            _lib.ptr(gy), gy.stride(0), _lib.ptr(x), x.stride(0), n, n_out, k, tps, _lib.ptr(part),
+            _lib.stream(part)), "dense_bwd_w_x6")
+        return ops.sum_rows(part).view(n_out, k)
     tiles = ((k + 31) // 32) * ((n_out + 31) // 32)
     slices = max(1, min((n + 31) // 32, -(-LINW_WG // tiles), LINW_MAX_SLICES))
     nps = -(-n // slices)

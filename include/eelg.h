@@ -280,6 +280,14 @@ typedef struct { int n_ins, max_jt, max_ut, max_rows; eelg_linw_ins ins[EELG_LIN
 int eelg_linear_bwd_w(const float* x, int x_row, const float* g, int g_row, int n_nodes,
                       int nodes_per_slice, float* partial, int n_partial, int w_total,
                       const eelg_linw_desc* desc, void* stream);
+/* Dense weight gradient (a Linear y = x W^T, x [n_rows, k] row stride ldx, g = dL/dy [n_rows,
+ * n_out] row stride ldg) on bf16 MFMA with fp32-accurate split operands (round 5; the weight
+ * gradients of the CGC models' Linear layers, cgc_modified.py:11-25):
+ * partial[s, j, kk] = sum over the rows r of split s (tiles_per_split 32-row tiles) of
+ * g[r, j] x[r, kk], s < ceil(ceil(n_rows / 32) / tiles_per_split); the caller sums over s
+ * (eelg_sum_rows) to grad W [n_out, k] in torch layout.  k in {32, 64, 96, 128}; -2 otherwise. */
+int eelg_linear_bwd_w_x6(const float* g, int ldg, const float* x, int ldx, int n_rows, int n_out,
+                         int k, int tiles_per_split, float* partial, void* stream);
 
 /* Radial MLP of the interaction block, fused (gnn/blocks.py:537-549, applied at :590):
  *   [Linear(n_feat -> hidden) + SiLU] + ([Linear(hidden -> hidden) + SiLU]) * (n_hidden - 1)

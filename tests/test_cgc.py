@@ -145,18 +145,22 @@ def test_cgc_model_fullsize_matches_oracle(variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n_out,bias", [(128, 256, True), (96, 192, False), (64, 21, True),
-                                          (32, 64, True), (5, 128, True)])
-def test_dense_linear_matches_torch(k, n_out, bias):
+@pytest.mark.parametrize("k,n_out,bias,rows", [(128, 256, True, 1000), (96, 192, False, 1000),
+                                               (64, 21, True, 1000), (32, 64, True, 1000),
+                                               (5, 128, True, 1000), (128, 256, True, 6000),
+                                               (96, 192, False, 4100), (64, 21, True, 5000),
+                                               (32, 300, True, 4096)])
+def test_dense_linear_matches_torch(k, n_out, bias, rows):
     """``gnn.dense.Linear`` (the CGC models' Linear layers on the in-tree MFMA kernels): output,
     grad-x, grad-W and grad-b against the fp64 torch Linear, 2e-6 of the largest entry (fp32
-    sums over K / over the rows)."""
+    sums over K / over the rows).  K >= 128 forward / grad-x and, from 4096 rows, the weight
+    gradient run on the split-bf16 kernels (ragged last row tile and output blocks included)."""
     from gnn import dense
     torch.manual_seed(3)
     ref = torch.nn.Linear(k, n_out, bias=bias).double()
     m = dense.Linear(k, n_out, bias=bias).cuda()
     m.load_state_dict({kk: v.float() for kk, v in ref.state_dict().items()})
-    x = torch.randn(1000, k, dtype=F64)
+    x = torch.randn(rows, k, dtype=F64)
     xo, xm = x.clone().requires_grad_(True), x.float().cuda().requires_grad_(True)
     yo, ym = ref(xo), m(xm)
     g = torch.randn_like(yo)
