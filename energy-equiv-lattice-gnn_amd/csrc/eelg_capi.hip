@@ -679,14 +679,15 @@ int eelg_segment_order_bwd(const float* src, const int* rowptr, const int* arg, 
 
 static int cgc_launch_fwd(const float* ps, const float* pr, const float* ep, const float* ef,
                           const float* ea, const int* sender, const int* rowptr,
-                          const float* row_scale, int n_nodes, int D, float* agg, void* stream) {
+                          const float* row_scale, int n_nodes, int D, float* agg, void* stream,
+                          const float* res = nullptr) {
   if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_fwd: D = %d > %d not built", D, EELG_CGC_MAXD);
   const dim3 g((n_nodes + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
 #define CGCF(C, E) hipLaunchKernelGGL((cgc_fwd_kernel<C, E>), g, dim3(256), 0, st, ps, pr, ep, ef, ea, \
-                                      sender, rowptr, row_scale, n_nodes, D, agg)
+                                      sender, rowptr, row_scale, n_nodes, D, agg, res)
   const int cpl = D > 128 ? 4 : D > 64 ? 2 : 1;
   if (ef) { if (cpl == 4) CGCF(4, true); else if (cpl == 2) CGCF(2, true); else CGCF(1, true); }
   else { if (cpl == 4) CGCF(4, false); else if (cpl == 2) CGCF(2, false); else CGCF(1, false); }
@@ -773,6 +774,13 @@ int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const flo
 int eelg_cgc_bwd_ef_parts(int n_nodes) {
   const int waves = (n_nodes + EELG_CGC_RPW - 1) / EELG_CGC_RPW;
   return n_nodes > 0 ? (waves + 3) / 4 : 0;
+}
+
+int eelg_cgc_fwd_ef_res(const float* ps, const float* pr, const float* ef, const float* ea,
+                        const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
+                        int D, const float* res, float* agg, void* stream) {
+  if (!ef || !ea) return fail(-2, "cgc_fwd_ef_res: ef and ea are required");
+  return cgc_launch_fwd(ps, pr, nullptr, ef, ea, sender, rowptr, row_scale, n_nodes, D, agg, stream, res);
 }
 
 int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
     const float* __restrict__ ef, const float* __restrict__ ea,
     const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
-    int n_nodes, int D, float* __restrict__ agg) {
+    int n_nodes, int D, float* __restrict__ agg, const float* __restrict__ res) {
   const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (node >= n_nodes) return;
@@ -132,9 +132,13 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
         for (int k = 0; k < CPL; ++k)
           acc[k] += cgc_softplus((zv[j][k] + pv[j][k]) + rv[k]) * cgc_sigmoid((zm[j][k] + pm[j][k]) + rm[k]);
   }
+  // the layer residual (h + conv(h), cgc_modified.py:77) added in the store (res may be NULL)
 #pragma unroll
   for (int k = 0; k < CPL; ++k)
-    if (lane + 64 * k < D) agg[(size_t)node * D + lane + 64 * k] = acc[k] * sc;
+    if (lane + 64 * k < D) {
+      const size_t o = (size_t)node * D + lane + 64 * k;
+      agg[o] = res ? acc[k] * sc + res[o] : acc[k] * sc;
+    }
 }
 
 // Backward: per receiver, recompute z_e and write dz_e = d msg / d z_e (.) g_n for every

@@ -46,6 +46,7 @@ _SIGS = {
     "eelg_cgc_fwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_cgc_bwd": ([_P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_cgc_fwd_ef": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P], _I),
+    "eelg_cgc_fwd_ef_res": ([_P] * 6 + [_P, _I, _I, _P, _P, _P], _I),
     "eelg_cgc_bwd_ef": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P], _I),
     "eelg_cgc_bwd_ef_parts": ([_I], _I),
     "eelg_csr_spmm": ([_P, _P, _P, _I, _P, _I, _I, _I, _P, _I, _I, _P], _I),

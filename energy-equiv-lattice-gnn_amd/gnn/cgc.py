@@ -14,6 +14,7 @@ the [E, 2D] edge projection is never written.
 """
 from __future__ import annotations
 
+import os
 from argparse import Namespace
 from typing import Dict, Optional
 
@@ -21,6 +22,9 @@ import torch
 
 from . import _lib, dense, ops
 from .blocks import EdgeIndex, as_csr, mat_square
+
+# the layer residual added inside the CGC kernels (1) or as a separate torch add (0)
+CGC_FUSED_RES = os.environ.get("EELG_CGC_FUSED_RES", "1") != "0"
 
 # Mandel 6x6 from the 21 upper-triangular outputs (cgc_modified.py:28-33)
 INDS_VAL = [[0, 1, 2, 3, 4, 5],
@@ -36,10 +40,10 @@ def _cgc_dw(x, gs, gr, db_on: bool):
     return dense.linear_bwd_w(x, gs), dense.linear_bwd_w(x, gr), (ops.sum_rows(gr) if db_on else None)
 
 
-def _cgc_dx(gs, gr, w, d):
-    """gs W_s + gr W_r: two launches of the linear kernel, the second adding the first in its
-    epilogue"""
-    dx = dense.linear_bwd_x(gs, w, 2 * d, d, w_off=0, ld=3 * d)
+def _cgc_dx(gs, gr, w, d, res=None):
+    """gs W_s + gr W_r (+ res, a residual's gradient): two launches of the linear kernel, each
+    adding the previous term in its epilogue"""
+    dx = dense.linear_bwd_x(gs, w, 2 * d, d, w_off=0, ld=3 * d, res=res)
     return dense.linear_bwd_x(gr, w, 2 * d, d, w_off=d, ld=3 * d, res=dx)
 
 
@@ -98,7 +102,10 @@ class _CGCConvEF(torch.autograd.Function):
     gradient is ef^T dz, read off the same dz the node blocks use."""
 
     @staticmethod
-    def forward(ctx, x, ea, wv, bv, wm, bm, ef, csr: ops.EdgeCSR, row_scale: Optional[torch.Tensor]):
+    def forward(ctx, x, ea, wv, bv, wm, bm, ef, csr: ops.EdgeCSR, row_scale: Optional[torch.Tensor],
+                residual: bool = False):
+        """``residual``: return x + conv(x) (the models' layer residual, cgc_modified.py:77), the
+        add done in the aggregation kernel's store and its gradient in grad-x's epilogue"""
         x = ops._f32(x).contiguous()
         ea = ops._f32(ea).contiguous()
         n, d = x.shape
@@ -111,13 +118,19 @@ class _CGCConvEF(torch.autograd.Function):
         pr = dense.linear_fwd(x, w, 2 * d, d, w_off=d, ld=3 * d, bias=b)
         agg = torch.empty(n, d, device=x.device, dtype=torch.float32)
         tok = ops.TIMER.start("cgc_fwd")
-        _lib.check(_lib.load().eelg_cgc_fwd_ef(
-            _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
-            _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(agg),
-            _lib.stream(agg)), "cgc_fwd_ef")
+        if residual:
+            _lib.check(_lib.load().eelg_cgc_fwd_ef_res(
+                _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
+                _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(x), _lib.ptr(agg),
+                _lib.stream(agg)), "cgc_fwd_ef_res")
+        else:
+            _lib.check(_lib.load().eelg_cgc_fwd_ef(
+                _lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ef), _lib.ptr(ea), _lib.ptr(csr.sender),
+                _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), _lib.ptr(row_scale), n, d, _lib.ptr(agg),
+                _lib.stream(agg)), "cgc_fwd_ef")
         ops.TIMER.stop(tok)
         ctx.save_for_backward(x, ea, ef, ps, pr, w, row_scale)
-        ctx.csr = csr
+        ctx.csr, ctx.residual = csr, residual
         return agg
 
     @staticmethod
@@ -144,8 +157,8 @@ class _CGCConvEF(torch.autograd.Function):
                          dea_part.new_zeros(2, 2 * d)])
         zero = torch.zeros(2 * d, d, device=x.device, dtype=torch.float32)
         dw = torch.cat([dws, dwr, zero], dim=1)                   # the edge block: through ea
-        dx = _cgc_dx(gs, gr, w, d)
-        return dx, dea, dw[:d], db[:d], dw[d:], db[d:], None, None, None
+        dx = _cgc_dx(gs, gr, w, d, g if ctx.residual else None)
+        return dx, dea, dw[:d], db[:d], dw[d:], db[d:], None, None, None, None
 
 
 def _edge_factor(edge_emb: torch.nn.Linear, we: torch.Tensor) -> torch.Tensor:
@@ -197,13 +210,14 @@ class CGCLayer(torch.nn.Module):
         return torch.cat([self.fc_values.weight[:, 2 * d:], self.fc_multip.weight[:, 2 * d:]])
 
     def forward_factored(self, x: torch.Tensor, csr: ops.EdgeCSR, ef: torch.Tensor,
-                         ea: torch.Tensor) -> torch.Tensor:
+                         ea: torch.Tensor, residual: bool = False) -> torch.Tensor:
         """The same layer on factored edge features (``_CGCConvEF``): ``ef`` [E, 8] =
-        [e5 | 1 | 0 | 0] in CSR order, ``ea`` = ``_edge_factor(edge embedding, edge_block())``."""
+        [e5 | 1 | 0 | 0] in CSR order, ``ea`` = ``_edge_factor(edge embedding, edge_block())``.
+        ``residual``: x + layer(x), added inside the kernels."""
         ops._require_device(x)
         return _CGCConvEF.apply(x, ea, self.fc_values.weight, self.fc_values.bias,
                                 self.fc_multip.weight, self.fc_multip.bias, ef, csr,
-                                self._scale(csr))
+                                self._scale(csr), residual)
 
 
 def _head(hidden: int) -> torch.nn.Sequential:
@@ -246,9 +260,13 @@ class _CGCBase(torch.nn.Module):
         ef = torch.cat([e5, torch.ones_like(e5[:, :1]), torch.zeros_like(e5[:, :2])], dim=1).contiguous()
         return csr, self.node_ft_embedding(node_in), ef
 
-    def _layer(self, i, h, csr, ef):
+    def _layer(self, i, h, csr, ef, residual: bool = False):
+        """layer i (h + layer_i(h) when ``residual``)"""
         layer = self.cgc_layers[i]
-        return layer.forward_factored(h, csr, ef, _edge_factor(self.edge_ft_embedding, layer.edge_block()))
+        ea = _edge_factor(self.edge_ft_embedding, layer.edge_block())
+        if residual and not CGC_FUSED_RES:
+            return h + layer.forward_factored(h, csr, ef, ea)
+        return layer.forward_factored(h, csr, ef, ea, residual)
 
     def _pool(self, h, batch):
         return ops.graph_pool(h, batch.batch, batch.num_graphs, self.global_reduction)
@@ -264,7 +282,7 @@ class CrystGraphConv(_CGCBase):
         csr, h, ef = self._encode(batch, batch.node_attrs)
         h = self._layer(0, h, csr, ef)
         for i in range(1, len(self.cgc_layers)):
-            h = h + self._layer(i, h, csr, ef)
+            h = self._layer(i, h, csr, ef, residual=True)   # h + layer_i(h)
         a = self.mlp(self._pool(h, batch))[:, self.inds_val]
         if self.params.positive == "square":
             return {"stiffness": mat_square(a)}
@@ -281,5 +299,5 @@ class CrystGraphConvVanilla(_CGCBase):
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         csr, h, ef = self._encode(batch, batch.positions)
         for i in range(len(self.cgc_layers)):
-            h = h + self._layer(i, h, csr, ef)
+            h = self._layer(i, h, csr, ef, residual=True)   # h + layer_i(h)
         return {"stiffness": self.mlp(self._pool(h, batch))}

@@ -191,6 +191,12 @@ int eelg_cgc_bwd(const float* ps, const float* pr, const float* ep, const int* s
 int eelg_cgc_fwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
                     const int* sender, const int* receiver, const int* rowptr,
                     const float* row_scale, int n_nodes, int D, float* agg, void* stream);
+/* The factored forward with the layer residual added in the store (round 5):
+ * agg[n] = row_scale[n] sum_e msg_e + res[n] (res [N, D], the layer input h of
+ * h + conv(h), cgc_modified.py:77 / cgc_vanilla.py:69; NULL: no residual). */
+int eelg_cgc_fwd_ef_res(const float* ps, const float* pr, const float* ef, const float* ea,
+                        const int* sender, const int* rowptr, const float* row_scale, int n_nodes,
+                        int D, const float* res, float* agg, void* stream);
 int eelg_cgc_bwd_ef(const float* ps, const float* pr, const float* ef, const float* ea,
                     const int* sender, const int* receiver, const int* rowptr,
                     const float* row_scale, int n_nodes, int D, const float* grad_agg, float* dz,

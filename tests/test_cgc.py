@@ -206,3 +206,37 @@ def test_cgc_factored_edges_match_generic_layer():
     a, r = run(True), run(False)
     for u, v in zip(a, r):
         assert _rel(u, v) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,reduction", [(128, "sum"), (64, "mean")])
+def test_cgc_fused_residual_matches_explicit_add(d, reduction):
+    """``forward_factored(..., residual=True)`` (x + layer(x) with the add in the aggregation
+    kernel's store and its gradient in grad-x's epilogue) equals the explicit ``x + layer(x)``:
+    output bitwise (one fp32 add either way), gradients within 1e-6 of their largest entry."""
+    from gnn import cgc
+    from gnn.model import EnergyEquivGNN
+    torch.manual_seed(5)
+    layer = cgc.CGCLayer(d, d, reduction).cuda()
+    emb = torch.nn.Linear(5, d).cuda()
+    b, _ = batch(3, 40, 160, 17)
+    bd = b.to("cuda")
+    csr = EnergyEquivGNN.edge_graph(bd)
+    e5 = cgc._edge_inputs(bd, csr)
+    ef = torch.cat([e5, torch.ones_like(e5[:, :1]), torch.zeros_like(e5[:, :2])], 1).contiguous()
+    x = torch.randn(csr.num_nodes, d, device="cuda")
+    g = torch.randn(csr.num_nodes, d, device="cuda")
+
+    def run(fused):
+        for p in list(layer.parameters()) + list(emb.parameters()):
+            p.grad = None
+        xr = x.clone().requires_grad_(True)
+        ea = cgc._edge_factor(emb, layer.edge_block())
+        y = layer.forward_factored(xr, csr, ef, ea, residual=True) if fused else \
+            xr + layer.forward_factored(xr, csr, ef, ea)
+        (y * g).sum().backward()
+        return [y.detach(), xr.grad] + [p.grad.clone() for p in list(layer.parameters()) + list(emb.parameters())]
+    a, r = run(True), run(False)
+    assert torch.equal(a[0], r[0])
+    for u, v in zip(a[1:], r[1:]):
+        assert _rel(u, v) < 1e-6
