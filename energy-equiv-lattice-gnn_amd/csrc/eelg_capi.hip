@@ -522,10 +522,10 @@ static const eelg_tp_cfg* tp_cfg(int cfg) {
 // node tiles of 2 * fwpb * nph receivers (fwpb waves x 2 half-waves); the tile count is rounded
 // up to a multiple of 8 so every tile's ngroups blocks land on one XCD, which takes a contiguous
 // range of tiles (see gen_kernels.py); surplus blocks exit
-static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes) {
+static dim3 tp_fwd_grid(const eelg_tp_cfg& c, int n_nodes, bool bf = false) {
   const int tn = 2 * c.fwpb * c.nph;
   const int tiles = (n_nodes + tn - 1) / tn;
-  return dim3(((tiles + 7) / 8) * 8 * c.ngroups);
+  return dim3(((tiles + 7) / 8) * 8 * (bf ? c.ngroups_bf : c.ngroups));
 }
 
 int eelg_tp_fwd(int cfg, const float* x, const float* sh, const float* w, const int* sender,
@@ -553,7 +553,7 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(sh) |
         reinterpret_cast<uintptr_t>(w)) & 15) != 0)
     return fail(-2, "tp_fwd_bf16: x, sh and w must be 16-byte aligned");
-  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes), dim3(64 * c->fwpb), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(c->fwd_bf, tp_fwd_grid(*c, n_nodes, true), dim3(64 * c->fwpb), 0, (hipStream_t)stream,
                      x, sh, static_cast<const unsigned short*>(w), sender, rowptr, n_nodes, inv_norm,
                      agg);
   return check_launch("tp_fwd_bf16");

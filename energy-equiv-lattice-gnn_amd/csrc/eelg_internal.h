@@ -39,6 +39,7 @@ struct eelg_tp_cfg {
   eelg_tp_bwd_bf_fn bwd_bf;
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
+  int ngroups_bf;            // path groups of the bf16-weight forward (its own accumulator cap)
 };
 
 struct eelg_sc_cfg {

@@ -39,6 +39,10 @@ TP_NPH = int(os.environ.get("EELG_TP_NPH", "8"))
 # lower bound of a forward that hands agg to a fused epilogue instead of HBM
 TP_FWD_NOSTORE = int(os.environ.get("EELG_TP_FWD_NOSTORE", "0"))
 TP_MAXACC = int(os.environ.get("EELG_TP_MAXACC", "64"))
+# the bf16-weight forward's path groups (config 5): smaller groups, 109 instead of 141 VGPRs.
+# r06d / r06e (lmax 3, 5k-node lattices): tp_fwd_tpB_l3_bw 0.477 -> 0.4985 of the roof; at 64
+# for fp32 (config 2: a cap of 40 took tp_fwd from 0.54 to 0.48, r06f)
+TP_MAXACC_BF = int(os.environ.get("EELG_TP_MAXACC_BF", "40"))
 # tp_fwd waves per workgroup (a node tile = 2 x TP_FWD_WPB x TP_NPH receivers; one-wave
 # workgroups refill a freed wave slot at once: r03z kbench 0.505 vs 0.520 ms at 4, 0.518 at 2;
 # in the step 0.438 vs 0.446 ms)
@@ -58,6 +62,10 @@ TP_FWD_WNT = int(os.environ.get("EELG_TP_FWD_WNT", "1"))
 # the kernel 3 % faster, the step 0.4 % slower as the following linear missed in L2; r04w: kbench
 # 0.491 -> 0.469 ms, but in the step the kernel itself 0.406 -> 0.418 ms and the step equal)
 TP_FWD_ANT = int(os.environ.get("EELG_TP_FWD_ANT", "0"))
+# LDS-DMA tp_fwd: edges in flight per half-wave (LDS image buffers), fp32 / bf16 weight storage
+TP_FWD_NBUF = int(os.environ.get("EELG_TP_FWD_NBUF", "2"))
+TP_FWD_NBUF_BF = int(os.environ.get("EELG_TP_FWD_NBUF_BF", "2"))
+
 TP_BWD_EPH = int(os.environ.get("EELG_TP_BWD_EPH", "1"))   # edges per half-wave in tp_bwd (4: 0.88 ms, 8: 0.90 ms vs 0.76 ms at 1)
 # tp_bwd: paths whose grad_agg slice + weight are in flight ahead of the path being computed
 # (r03v: 1: 0.781 ms, 2: 0.713, 3: 0.727)
@@ -413,6 +421,8 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     its lanes."""
     WPB = TP_FWD_WPB
     TN = 2 * WPB * TP_NPH
+    NBUF = TP_FWD_NBUF_BF if bf else TP_FWD_NBUF
+    assert NBUF >= 2
     CG, LW = _chan_groups()
     ng = len(groups) * CG                 # blocks per node tile: (path group, channel group)
     glists = [_glds_chunks(groups, nshp, node_off, 2 if bf else 4, c) for c in range(CG)]
@@ -425,7 +435,7 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ rowptr, int n_nodes,")
     L.append("    float inv_norm, float* __restrict__ agg) {")
-    L.append(f"  __shared__ float4 img_[{WPB}][2][2][{NI}];   // [wave][buffer][half][chunk]")
+    L.append(f"  __shared__ float4 img_[{WPB}][{NBUF}][2][{NI}];   // [wave][buffer][half][chunk]")
     L.append("  const int lane = threadIdx.x & 63, hf = lane >> 5;")
     L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
     L.append("  const int u = lane & 31;")
@@ -477,12 +487,12 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
                + [f"y{l * l + j}" for l in need_l2 for j in range(2 * l + 1)]
                + [f"w{p.slot}" for p in grp])
         L.append("    float " + ", ".join(f"{a} = 0.0f" for a in accs) + ";")
-        L += issue("0", 0)
-        L += issue("1", 1)
+        for k in range(NBUF):
+            L += issue(str(k), k)
         L.append("    int b = 0;")
         L.append("    for (;;) {")
-        # edge e's rows: everything but the last edge's LDS-DMA instructions has landed
-        L.append(f'      asm volatile("s_waitcnt vmcnt({2 * nj})" ::: "memory");')
+        # edge e's rows: everything but the later edges' LDS-DMA instructions has landed
+        L.append(f'      asm volatile("s_waitcnt vmcnt({(NBUF - 1) * 2 * nj})" ::: "memory");')
         # the LDS reads are inline asm: hipcc would otherwise order every LDS read after ALL
         # outstanding LDS-DMA (a vmcnt(0): it cannot tell the image being read from the one
         # being filled), which would retire edge e+2's rows too
@@ -550,9 +560,9 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
             L.append(f"        ++node_{h}; nend_{h} = nend2_{h}; nend2_{h} = rowptr[min(node_{h} + 2, n1_{h})];")
             L.append("      }")
         L.append("      if (e_0 >= eend_0 && e_1 >= eend_1) break;")
-        L += ["  " + ln for ln in issue("b", 2)]
+        L += ["  " + ln for ln in issue("b", NBUF)]
         L += _glds_compute(grp, cur, accs)
-        L.append("      ++e_0; ++e_1; b ^= 1;")
+        L.append("      ++e_0; ++e_1; " + ("b ^= 1;" if NBUF == 2 else f"b = b == {NBUF - 1} ? 0 : b + 1;"))
         L.append("    }")
         L.append('    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the wave')
         L.append("    break; }")
@@ -578,7 +588,7 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     wn = sum(p.mul for p in paths)
     for p in paths:
         assert p.mul == MUL
-    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), TP_MAXACC)
+    groups = _group_paths(sorted(paths, key=lambda p: (p.l1, p.l2, p.l3)), TP_MAXACC_BF if bf else TP_MAXACC)
     node_ls = [ir.l for _, ir in node]
     node_off = {ir.l: o for (m, ir), o in zip(node, node.offsets())}
     L: List[str] = []
@@ -1882,8 +1892,11 @@ def main(outdir: str) -> None:
         for name, (node, sh, target) in tp_configs().items():
             code, info = emit_tp(name + sfx, node, sh, target)
             parts.append(code)
+            info["ngroups_bf"] = 0
             if bf:
-                parts.append(emit_tp(name + sfx, node, sh, target, "bf16")[0])
+                code_bf, info_bf = emit_tp(name + sfx, node, sh, target, "bf16")
+                parts.append(code_bf)
+                info["ngroups_bf"] = info_bf["ngroups"]
             tp_table.append((name + sfx, info))
         for name, (coupling, ls, corr) in sc_configs().items():
             code, info = emit_sc(name + sfx, coupling, ls, corr)
@@ -1898,7 +1911,7 @@ def main(outdir: str) -> None:
                    else f"nullptr, nullptr, tp_bws_{name}, nullptr")
             parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                          f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                         f'{bfk}}},')
+                         f'{bfk}, {i["ngroups_bf"]}}},')
         parts.append("};")
         parts.append("static const eelg_sc_cfg kScConfigs[] = {")
         for name, i in sc_table:
