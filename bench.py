@@ -229,11 +229,12 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax:
                                         "steps: bench.py --cpu-full)")}
 
 
-def cgc_fwd_bytes(n: int, e: int, d: int) -> int:
+def cgc_fwd_bytes(n: int, e: int, d: int, residual: bool = False) -> int:
     """Algorithmic bytes of one fused CGC edge-conv launch on factored edge features
     (``eelg_cgc_fwd_ef``, the models' path): node projections ps, pr [N, 2D] read once, the
-    8-float edge rows ef [E, 8] and A [8, 2D], sender [E] + rowptr [N+1], agg [N, D] written."""
-    return 4 * (2 * n * 2 * d + e * 8 + 8 * 2 * d + e + (n + 1) + n * d)
+    8-float edge rows ef [E, 8] and A [8, 2D], sender [E] + rowptr [N+1], agg [N, D] written;
+    with the layer residual (``eelg_cgc_fwd_ef_res``) the layer input h [N, D] is read too."""
+    return 4 * (2 * n * 2 * d + e * 8 + 8 * 2 * d + e + (n + 1) + n * d + (n * d if residual else 0))
 
 
 def cpu_baseline_cgc(modified: bool, p, n_nodes: int, n_edges: int, budget_s: float):
@@ -321,15 +322,20 @@ def main_cgc(args):
     if rank == 0:
         n_tot, e_tot = args.batch * args.nodes, args.batch * args.edges
         roof = None
-        if "cgc_fwd" in ksum:
-            byts = cgc_fwd_bytes(n_tot, e_tot, hid)
-            ms = ksum["cgc_fwd"]["mean_ms"]
+        if "cgc_fwd" in ksum or "cgc_fwd_res" in ksum:
+            # the layers with the residual in the store (cgc_fwd_res) read h as well: the
+            # launch-weighted bytes over the launch-weighted time of both
+            parts = [(ksum[k]["count"], cgc_fwd_bytes(n_tot, e_tot, hid, k == "cgc_fwd_res"),
+                      ksum[k]["mean_ms"]) for k in ("cgc_fwd", "cgc_fwd_res") if k in ksum]
+            cnt = sum(c for c, _, _ in parts)
+            byts = round(sum(c * b for c, b, _ in parts) / cnt)
+            ms = sum(c * m for c, _, m in parts) / cnt
             ach = byts / (ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                     "traffic_detail": pmc_traffic("cgc_fwd_kernel", args),
                     "kernel": "cgc_fwd (fused gather + factored edge projection + softplus*sigmoid + segmented sum)",
-                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum["cgc_fwd"]["count"]}
+                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": cnt}
             if roof["traffic_detail"]:
                 roof["traffic"] = roof["traffic_detail"]["bytes"]
                 roof["traffic_detail"]["ratio_to_algorithmic"] = round(roof["traffic"] / byts, 3)

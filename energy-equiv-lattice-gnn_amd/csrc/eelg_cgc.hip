@@ -137,7 +137,8 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
   for (int k = 0; k < CPL; ++k)
     if (lane + 64 * k < D) {
       const size_t o = (size_t)node * D + lane + 64 * k;
-      agg[o] = res ? acc[k] * sc + res[o] : acc[k] * sc;
+      // two roundings, as h + (sc * sum) in torch: no contraction into one fma
+      agg[o] = res ? __fadd_rn(__fmul_rn(acc[k], sc), res[o]) : acc[k] * sc;
     }
 }
 
