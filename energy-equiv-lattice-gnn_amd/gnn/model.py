@@ -141,13 +141,37 @@ class GNN_Head(torch.nn.Module):  # noqa: N801
         return self.positive_layer(self.cart_to_Mandel(stiff))
 
 
+class _Embed1(torch.autograd.Function):
+    """y = b + a w^T for one input feature a [N, 1]: forward torch.addcmul, backward the two
+    column sums on ``ops.sum_rows`` (deterministic; torch's reductions were 2 x 33 us per step
+    at [32768, 32], r06i).  No gradient w.r.t. the node attributes (data)."""
+
+    @staticmethod
+    def forward(ctx, attrs, weight, bias):
+        ctx.save_for_backward(attrs)
+        ctx.has_bias = bias is not None
+        w = weight[:, 0]
+        return torch.addcmul(bias, attrs, w) if bias is not None else attrs * w
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import ops
+        (attrs,) = ctx.saved_tensors
+        gy = ops._f32(gy).contiguous()
+        gw = ops.sum_rows(gy * attrs).unsqueeze(1) if ctx.needs_input_grad[1] else None
+        gb = ops.sum_rows(gy) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return None, gw, gb
+
+
 def _embed(lin: torch.nn.Linear, attrs: torch.Tensor) -> torch.Tensor:
     """``Linear(1 -> 32)`` of the node attributes (``gnn/model.py:122,142``).  With one input
     feature it is an outer product plus bias: one broadcast multiply-add instead of a K = 1
     library GEMM (0.19 ms per step on MI355X for [32768 x 1] x [1 x 32], r02q), and its weight
-    gradient is a column sum.  Same values (a single product per output plus the bias)."""
+    and bias gradients are column sums.  Same values (a single product per output plus the bias)."""
     if lin.in_features != 1:
         return lin(attrs)
+    if attrs.is_cuda and not attrs.requires_grad:
+        return _Embed1.apply(attrs, lin.weight, lin.bias)
     return torch.addcmul(lin.bias, attrs, lin.weight[:, 0]) if lin.bias is not None \
         else attrs * lin.weight[:, 0]
 
