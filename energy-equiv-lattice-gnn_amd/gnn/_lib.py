@@ -55,6 +55,9 @@ _SIGS = {
     "eelg_sc_bwd_x_cm": ([_I, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
     "eelg_sc_cmajor": ([_I, _I, _P, _I, _I, _P, _P], _I),
+    "eelg_scg_fwd": ([_P, _P, _P, _I, _P, _I, _I, _P, _I, _P], _I),
+    "eelg_scg_bwd_x": ([_P, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P], _I),
+    "eelg_scg_bwd_coef": ([_P, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P], _I),
     "eelg_linear_fwd": ([_P, _I, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_fwd_res": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _P], _I),
     "eelg_linear_bwd_w": ([_P, _I, _P, _I, _I, _I, _P, _I, _I, _P, _P], _I),
@@ -108,6 +111,16 @@ GATE_MAXGATES = 512
 class GateDesc(ctypes.Structure):
     _fields_ = [("n_scal", _I), ("n_gates", _I), ("n_blk", _I), ("pad", _I),
                 ("blk_mul", _I * GATE_MAXBLK), ("blk_dim", _I * GATE_MAXBLK)]
+
+
+SCG_MAXD = 25            # include/eelg.h EELG_SCG_MAXD / EELG_SCG_CHUNK
+SCG_CHUNK = 512
+
+
+class ScgDesc(ctypes.Structure):
+    _fields_ = [("D", _I), ("Dout", _I), ("mul", _I), ("nterms", _I),
+                ("xb", _I * SCG_MAXD), ("xs", _I * SCG_MAXD), ("ob", _I * SCG_MAXD),
+                ("os", _I * SCG_MAXD), ("orow", _I * (SCG_MAXD + 1))]
 
 
 class RadialDesc(ctypes.Structure):

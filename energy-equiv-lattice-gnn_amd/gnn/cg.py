@@ -195,14 +195,23 @@ def tp_paths(node_irreps: Irreps, sh_irreps: Irreps, target: Irreps) -> List[TPP
 # --------------------------------------------------------------------------
 # MACE U matrices and their symmetrised sparse form
 # --------------------------------------------------------------------------
+# correlation 4: the reference couples through natural-parity irreps up to l = 11 only
+# (``filter_ir_mid``, gnn/mace.py:444-458, applied at every coupling level, gnn/mace.py:392-393)
+MID_FILTER_LMAX = 11
+
+
+def _mid_ok(ir: Ir) -> bool:
+    return ir.l <= MID_FILTER_LMAX and ir.p == (-1) ** ir.l
+
+
 @functools.lru_cache(maxsize=None)
-def _coupled(irs: Tuple[Ir, ...], nu: int, only=None):
+def _coupled(irs: Tuple[Ir, ...], nu: int, only=None, mid_filter: bool = False):
     """``_wigner_nj`` over ``nu`` copies of the (mul=1) coupling irreps.
 
     Returns [(ir_out, E)] with E of shape [ir_out.dim, D, ..., D] (nu copies of
     D = sum dims), stably sorted by irrep like ``gnn/mace.py:432``.  ``only``
     keeps just one output irrep at the last level (same relative order, since the
-    sort is stable)."""
+    sort is stable).  ``mid_filter``: the correlation-4 ``filter_ir_mid`` at every level."""
     D = sum(ir.dim for ir in irs)
     if nu == 1:
         eye, out, s = np.eye(D), [], 0
@@ -211,11 +220,13 @@ def _coupled(irs: Tuple[Ir, ...], nu: int, only=None):
             s += ir.dim
         return tuple(x for x in out if only is None or x[0] == only)
     out = []
-    for ir_l, c_l in _coupled(irs, nu - 1):
+    for ir_l, c_l in _coupled(irs, nu - 1, None, mid_filter):
         s = 0
         for ir in irs:
             for ir_o in ir_l.times(ir):
                 if only is not None and ir_o != only:
+                    continue
+                if mid_filter and not _mid_ok(ir_o):
                     continue
                 w = wigner_3j(ir_o.l, ir_l.l, ir.l) * math.sqrt(ir_o.dim)
                 t = np.einsum("jk,ijl->ikl", c_l.reshape(ir_l.dim, -1), w)
@@ -231,14 +242,16 @@ def U_matrix(coupling: str, l_out: int, nu: int) -> np.ndarray:
     """U_nu for output irrep l_out (natural parity): [2l+1, D x nu, K_nu]."""
     irs = tuple(ir for _, ir in Irreps(coupling))
     target = Ir(l_out, (-1) ** l_out)
-    mats = [e for ir, e in _coupled(irs, nu, target) if ir == target]
+    # U_matrix_real(correlation=nu) filters the intermediate irreps iff nu == 4 (gnn/mace.py:444)
+    mats = [e for ir, e in _coupled(irs, nu, target, nu == 4) if ir == target]
     return np.stack(mats, axis=-1)
 
 
 class SymConPlan(NamedTuple):
     """Sparse polynomial form of MACE's SymmetricContraction for one irreps config.
 
-    ``terms`` lists (degree, (a, b, c), out) with a<=b<=c (unused slots -1) and
+    ``terms`` lists (degree, (a, b, c), out) with a<=b<=c (unused slots -1; correlation 4:
+    four slots (a, b, c, d), ordered by ``out``) and
     ``out`` in 0..D-1 (the [L][M] output component).  ``ubig`` [nnz, K_total]
     maps the stacked weights (order: for L: W1, W2, W3 ... per ``weight_blocks``)
     to the per-term coefficients: coef[term, c] = (ubig @ W_all)[term, c]."""
@@ -265,6 +278,7 @@ def symcon_plan(coupling: str, out_ls: Tuple[int, ...], correlation: int) -> Sym
     Dout = off
     blocks, cols = [], {}
     kt = 0
+    slots = max(3, correlation)    # monomial index slots of a term (unused: -1)
     for l in out_ls:
         for nu in range(1, correlation + 1):
             k = U_matrix(coupling, l, nu).shape[-1]
@@ -283,7 +297,7 @@ def symcon_plan(coupling: str, out_ls: Tuple[int, ...], correlation: int) -> Sym
                     acc += u[(slice(None),) + p]
                 for m in range(2 * l + 1):
                     if np.abs(acc[m]).max() > 1e-12:
-                        key = (nu, tuple(cls) + (-1,) * (3 - nu), ls_out_off[l] + m)
+                        key = (nu, tuple(cls) + (-1,) * (slots - nu), ls_out_off[l] + m)
                         r = np.zeros(kt)
                         r[k0: k0 + k] = acc[m]
                         rows[key] = r
@@ -295,7 +309,12 @@ def symcon_plan(coupling: str, out_ls: Tuple[int, ...], correlation: int) -> Sym
             return (0, a, 0, 0, 0, o)
         return (1, a, b, 0 if nu == 2 else 1, c, o)
 
-    keys = sorted(rows, key=order)
+    def order_by_output(key):
+        # correlation 4 (the generic kernels, csrc/eelg_scg.hip): grouped by output component
+        nu, cls, o = key
+        return (o, nu, cls)
+
+    keys = sorted(rows, key=order if correlation <= 3 else order_by_output)
     ubig = np.stack([rows[k] for k in keys]) if keys else np.zeros((0, kt))
     return SymConPlan(Dout, tuple(out_ls), tuple(keys), ubig, tuple(blocks))
 

@@ -8,7 +8,10 @@ Reference ``params`` space (``gnn/model.py:31-42``, ``gnn/mace.py:112-177``): ``
 
 * tensor product: SH lmax 1..4, node irreps ``{mul}x0e`` (first layer) or the natural-parity
   hidden irreps ``{mul}x0e+{mul}x1o+...`` up to the SH lmax (later layers);
-* symmetric contraction: the same lmax, outputs = those hidden irreps, correlation 1..3;
+* symmetric contraction: the same lmax, outputs = those hidden irreps, correlation 1..3
+  generated; correlation 4 (the reference's ``filter_ir_mid`` coupling) runs the table-driven
+  kernels (``csrc/eelg_scg.hip``) for SH lmax <= 3 (``TABLE_LMAX``: at lmax 4 the reference's
+  own ``U_matrix_4`` is a [9, 25, 25, 25, 25, K] tensor, gigabytes, and so is its host build);
 * ``mul`` (channels per irrep) in ``MULS``: one lane per channel in the interaction kernels, a
   half-wave per 32 channels (mul = 64: two channel groups; mul = 16: half a half-wave).  The
   reference default and the benchmark configurations are 32; bf16 storage of the edge tensors
@@ -22,6 +25,8 @@ MUL = 32
 MULS = (16, 32, 64)
 LMAX = (1, 2, 3, 4)
 CORRELATIONS = (1, 2, 3)
+TABLE_CORRELATIONS = (4,)
+TABLE_LMAX = 3
 
 
 def natural(l: int) -> str:
@@ -39,7 +44,8 @@ def coupling_str(lmax: int) -> str:
 def supported_text() -> str:
     return (f"generated kernel sets: SH lmax in {LMAX} with hidden_irreps "
             f"'{hidden_irreps_str(1)}' .. '{hidden_irreps_str(4)}' (mul channels of every l up to "
-            f"the SH lmax, mul in {MULS}), correlation in {CORRELATIONS}")
+            f"the SH lmax, mul in {MULS}), correlation in {CORRELATIONS}; correlation "
+            f"{TABLE_CORRELATIONS[0]} (table-driven) for SH lmax <= {TABLE_LMAX}")
 
 
 def mul_of(irreps) -> int:
@@ -62,11 +68,13 @@ def check_tp(node, sh, target) -> None:
 
 
 def check_sc(irreps_in, ls: Tuple[int, ...], correlation: int) -> None:
-    """Raise NotImplementedError unless the symmetric contraction is a generated set."""
+    """Raise NotImplementedError unless the symmetric contraction is a generated set (or a
+    table-driven one: correlation 4)."""
     lmax = irreps_in.lmax
     mul = mul_of(irreps_in)
     ok = (lmax in LMAX and mul in MULS and str(irreps_in) == hidden_irreps_str(lmax, mul)
-          and tuple(ls) == tuple(range(lmax + 1)) and correlation in CORRELATIONS)
+          and tuple(ls) == tuple(range(lmax + 1))
+          and (correlation in CORRELATIONS or (correlation in TABLE_CORRELATIONS and lmax <= TABLE_LMAX)))
     if not ok:
         raise NotImplementedError(
             f"no HIP symmetric-contraction kernels for {irreps_in} -> l in {tuple(ls)}, "
@@ -81,3 +89,8 @@ def coupling_target(lmax: int, mul: int = MUL) -> str:
 def _sh(lmax: int):
     from .irreps import Irreps
     return Irreps.spherical_harmonics(lmax)
+
+
+def table_driven(correlation: int) -> bool:
+    """the contraction runs the table-driven kernels (eelg_scg_*) instead of a generated set"""
+    return correlation in TABLE_CORRELATIONS

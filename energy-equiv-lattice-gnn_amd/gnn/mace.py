@@ -99,7 +99,10 @@ class SymmetricContraction(torch.nn.Module):
         # fail at construction, with the supported list, for structures without generated kernels
         kernel_sets.check_sc(self.irreps_in, tuple(ir.l for _, ir in self.irreps_out), correlation)
         plan = cg.symcon_plan(coupling, ls, correlation)
-        self._sig = cg.fnv1a64(cg.sc_signature(coupling, ls, correlation))
+        # correlation 4: the table-driven kernels (csrc/eelg_scg.hip) over the same plan
+        self._table = (ops.ScgTable(plan, tuple(ir.l for _, ir in self.irreps_in), ls, self.mul)
+                       if kernel_sets.table_driven(correlation) else None)
+        self._sig = None if self._table else cg.fnv1a64(cg.sc_signature(coupling, ls, correlation))
         self.block_order = [(l, nu) for l, nu, _ in plan.weight_blocks]
         ks = {}
         for l, nu, k in plan.weight_blocks:
@@ -198,8 +201,8 @@ class SymmetricContraction(torch.nn.Module):
         if self.u_sym.is_cuda:
             if getattr(self, "_u_csr", None) is None:
                 self._u_csr = ops.SparseRows(self.u_sym)
-            return ops.symcon_coefficients(self.weight_matrix(), self._u_csr,
-                                           self._config()[1]["coef_ld"])
+            ld = self._table.ldc if self._table else self._config()[1]["coef_ld"]
+            return ops.symcon_coefficients(self.weight_matrix(), self._u_csr, ld)
         return torch.matmul(self.u_sym, self.weight_matrix()).t().contiguous()
 
     def forward(self, x: torch.Tensor, y: torch.Tensor = None) -> torch.Tensor:
@@ -214,6 +217,15 @@ class SymmetricContraction(torch.nn.Module):
                                       "on the hot path: the model passes y=None (gnn/blocks.py:486)")
         if x.dim() == 3:
             x = unreshape_irreps(self.irreps_in, x)
+        if self._table is not None:
+            ahead, self._ahead = self._ahead, None
+            if ahead is not None:
+                coef = ahead[0]
+                torch.cuda.current_stream(x.device).wait_event(ahead[1])
+                coef.record_stream(torch.cuda.current_stream(x.device))
+            else:
+                coef = self.coefficients()
+            return ops.symmetric_contraction_table(x, coef, self._table)
         idx, info = self._config()
         side = ops.side_stream(x.device, 1) if (ops.OVERLAP and x.is_cuda) else None
         if side is None:

@@ -506,6 +506,103 @@ def symmetric_contraction(x, coef, cfg: int, info: Dict[str, int], mul: int, sid
     return _SymCon.apply(x, coef, cfg, info, mul, side)
 
 
+class ScgTable:
+    """Term table of a symmetric contraction for the table-driven kernels (``eelg_scg_*``,
+    correlation 4): ``plan`` = ``cg.symcon_plan`` (terms sorted by output component), ``ls_in``
+    / ``ls_out`` the coupling / output l's (one block of ``mul`` channels each, mul-major)."""
+
+    def __init__(self, plan, ls_in, ls_out, mul: int):
+        d = _lib.ScgDesc()
+        D = sum(2 * l + 1 for l in ls_in)
+        Dout = sum(2 * l + 1 for l in ls_out)
+        if D > _lib.SCG_MAXD or Dout > _lib.SCG_MAXD:
+            raise NotImplementedError(f"table-driven contraction: {D} / {Dout} components per channel "
+                                      f"(at most {_lib.SCG_MAXD})")
+        d.D, d.Dout, d.mul, d.nterms = D, Dout, mul, len(plan.terms)
+
+        def layout(ls, base, stride):
+            a, off = 0, 0
+            for l in ls:
+                for m in range(2 * l + 1):
+                    base[a], stride[a] = mul * off + m, 2 * l + 1
+                    a += 1
+                off += 2 * l + 1
+        layout(ls_in, d.xb, d.xs)
+        layout(ls_out, d.ob, d.os)
+        self.ldc = max(64, -(-len(plan.terms) // 64) * 64)
+        packed, outs = [], []
+        for q, (nu, cls, o) in enumerate(plan.terms):
+            idx = [i if i >= 0 else D for i in cls] + [D] * (4 - len(cls))
+            if len(idx) != 4:
+                raise ValueError(f"term {cls}: more than four factors")
+            packed.append(idx[0] | idx[1] << 8 | idx[2] << 16 | idx[3] << 24)
+            outs.append(o)
+        if outs != sorted(outs):
+            raise ValueError("table-driven contraction: terms must be sorted by output component")
+        for q in range(Dout + 1):
+            d.orow[q] = sum(1 for o in outs if o < q)
+        pad = self.ldc - len(packed)
+        packed += [D | D << 8 | D << 16 | D << 24] * pad
+        outs += [Dout] * pad
+        self.desc, self.D, self.Dout, self.mul = d, D, Dout, mul
+        self._terms = torch.tensor(packed, dtype=torch.int64).to(torch.int32)
+        self._outs = torch.tensor(outs, dtype=torch.int32)
+        self._dev = {}
+
+    def on(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = (self._terms.to(device), self._outs.to(device))
+        return self._dev[key]
+
+
+class _SymConTable(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, coef, tab: ScgTable):
+        x, coef = _f32(x), _f32(coef)
+        n = x.shape[0]
+        if x.shape[1] != tab.mul * tab.D or coef.shape != (tab.mul, tab.ldc):
+            raise ValueError(f"shape mismatch: x {tuple(x.shape)} coef {tuple(coef.shape)} vs mul "
+                             f"{tab.mul}, D {tab.D}, ldc {tab.ldc}")
+        terms, _ = tab.on(x.device)
+        out = torch.empty(n, tab.mul * tab.Dout, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().eelg_scg_fwd(ctypes.byref(tab.desc), _lib.ptr(terms), _lib.ptr(x), x.shape[1],
+                                            _lib.ptr(coef), tab.ldc, n, _lib.ptr(out), out.shape[1],
+                                            _lib.stream(out)), "scg_fwd")
+        ctx.save_for_backward(x, coef)
+        ctx.tab = tab
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, coef = ctx.saved_tensors
+        tab = ctx.tab
+        g = _f32(g)
+        n = x.shape[0]
+        lib = _lib.load()
+        terms, outs = tab.on(x.device)
+        gx = gcoef = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            _lib.check(lib.eelg_scg_bwd_x(ctypes.byref(tab.desc), _lib.ptr(terms), _lib.ptr(x), x.shape[1],
+                                          _lib.ptr(coef), tab.ldc, _lib.ptr(g), g.shape[1], n, _lib.ptr(gx),
+                                          _lib.stream(gx)), "scg_bwd_x")
+        if ctx.needs_input_grad[1]:
+            nch = max(1, -(-n // _lib.SCG_CHUNK))
+            part = torch.zeros(nch, tab.mul, tab.ldc, device=x.device, dtype=torch.float32)
+            _lib.check(lib.eelg_scg_bwd_coef(ctypes.byref(tab.desc), _lib.ptr(terms), _lib.ptr(outs), tab.ldc,
+                                             _lib.ptr(x), x.shape[1], _lib.ptr(g), g.shape[1], n,
+                                             _lib.ptr(part), _lib.stream(part)), "scg_bwd_coef")
+            gcoef = sum_rows(part)
+        return gx, gcoef, None
+
+
+def symmetric_contraction_table(x, coef, tab: ScgTable):
+    """The table-driven contraction (correlation 4): ``x`` [N, mul*D] rows, ``coef`` [mul, tab.ldc]."""
+    _require_device(x, coef)
+    return _SymConTable.apply(x, coef, tab)
+
+
 class _nullctx:
     def __enter__(self):
         return None

@@ -244,6 +244,30 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes,
                      int mul, int chunk, float* partial, void* stream);
 
+/* Symmetric contraction from a term table (correlation 4: U_matrix_real with filter_ir_mid,
+ * gnn/mace.py:435-477; the contraction itself gnn/mace.py:242-277).  Replaces
+ * SymmetricContraction.forward for the structures without generated kernels.
+ * terms[t]: four 8-bit component indices (slot k at bits 8k; an unused slot = D, a constant 1),
+ * sorted by output component, desc.orow[q] .. orow[q+1]-1 the terms of output q.  Component a of
+ * channel c of node n: x[n*ldx + xb[a] + c*xs[a]]; outputs likewise (ob, os, ldo).
+ * coef [mul, ldc], ldc a multiple of 64 >= nterms.  eelg_scg_bwd_coef writes deterministic
+ * partials [ceil(n_nodes / EELG_SCG_CHUNK), mul, ldc] (term_out[t]: output of term t; padding
+ * terms t >= nterms need indices D and output Dout: they produce 0); the caller sums them. */
+#define EELG_SCG_MAXD 25
+#define EELG_SCG_CHUNK 512
+typedef struct {
+  int D, Dout, mul, nterms;
+  int xb[EELG_SCG_MAXD], xs[EELG_SCG_MAXD];
+  int ob[EELG_SCG_MAXD], os[EELG_SCG_MAXD];
+  int orow[EELG_SCG_MAXD + 1];
+} eelg_scg_desc;
+int eelg_scg_fwd(const eelg_scg_desc* d, const unsigned* terms, const float* x, int ldx, const float* coef,
+                 int ldc, int n_nodes, float* out, int ldo, void* stream);
+int eelg_scg_bwd_x(const eelg_scg_desc* d, const unsigned* terms, const float* x, int ldx, const float* coef,
+                   int ldc, const float* grad_out, int ldg, int n_nodes, float* grad_x, void* stream);
+int eelg_scg_bwd_coef(const eelg_scg_desc* d, const unsigned* terms, const int* term_out, int ldc, const float* x,
+                      int ldx, const float* grad_out, int ldg, int n_nodes, float* partial, void* stream);
+
 /* Channel-mixing linear on mul-major irreps rows (o3.Linear, gnn/blocks.py:516-521,
  * 553-559,471-476; gnn/model.py:82-86), fp32 MFMA.  A descriptor lists output
  * slots; each slot sums alpha * x_block @ W over its sources, W element

@@ -59,23 +59,27 @@ def get_edge_vectors_and_lengths(positions, edge_index, shifts, normalize=False,
     return vectors, lengths
 
 
-def _wigner_nj(irrepss, dtype=torch.float64):
-    """``gnn/mace.py:363-432`` (normalization='component', no filter)."""
+# ``filter_ir_mid`` of U_matrix_real for correlation 4 (gnn/mace.py:444-458): natural parity, l <= 11
+_FILTER_MID_C4 = tuple((l, 1 if l % 2 == 0 else -1) for l in range(12))
+
+
+def _wigner_nj(irrepss, dtype=torch.float64, filter_ir_mid=None):
+    """``gnn/mace.py:363-432`` (normalization='component')."""
     irrepss = [Irreps(x) for x in irrepss]
     names = {str(x) for x in irrepss}
     if len(names) == 1 and dtype == torch.float64:
         # n copies of one irreps (every U_matrix_real call): memoised per process, the
         # result is shared by every output irrep and contraction of that coupling
-        return list(_wigner_nj_same(names.pop(), len(irrepss)))
-    return _wigner_nj_impl(irrepss, dtype)
+        return list(_wigner_nj_same(names.pop(), len(irrepss), filter_ir_mid))
+    return _wigner_nj_impl(irrepss, dtype, filter_ir_mid)
 
 
 @functools.lru_cache(maxsize=None)
-def _wigner_nj_same(irreps: str, n: int):
-    return tuple(_wigner_nj_impl([Irreps(irreps)] * n, torch.float64))
+def _wigner_nj_same(irreps: str, n: int, filter_ir_mid=None):
+    return tuple(_wigner_nj_impl([Irreps(irreps)] * n, torch.float64, filter_ir_mid))
 
 
-def _wigner_nj_impl(irrepss, dtype):
+def _wigner_nj_impl(irrepss, dtype, filter_ir_mid=None):
     if len(irrepss) == 1:
         (irreps,) = irrepss
         ret, e, i = [], torch.eye(irreps.dim, dtype=dtype), 0
@@ -87,10 +91,12 @@ def _wigner_nj_impl(irrepss, dtype):
         return ret
     *left, right = irrepss
     ret = []
-    for ir_left, path_left, c_left in _wigner_nj(left, dtype):
+    for ir_left, path_left, c_left in _wigner_nj(left, dtype, filter_ir_mid):
         i = 0
         for mul, ir in right:
             for ir_out in ir_left * ir:
+                if filter_ir_mid is not None and (ir_out.l, ir_out.p) not in filter_ir_mid:
+                    continue
                 c = wigner_3j(ir_out.l, ir_left.l, ir.l, dtype=dtype) * ir_out.dim ** 0.5
                 c = torch.einsum("jk,ijl->ikl", c_left.flatten(1), c)
                 c = c.reshape(ir_out.dim, *(x.dim for x in left), ir.dim)
@@ -106,7 +112,7 @@ def _wigner_nj_impl(irrepss, dtype):
 
 
 def U_matrix_real(irreps_in, irreps_out, correlation: int, dtype=torch.float64):
-    """``gnn/mace.py:435-477`` (correlation <= 3, so no filter_ir_mid)."""
+    """``gnn/mace.py:435-477`` (correlation 4 couples through ``filter_ir_mid``, :444-458)."""
     ir, u = _U_matrix_real_cached(str(Irreps(irreps_in)), str(Irreps(irreps_out)), correlation)
     return [ir, u.to(dtype).clone()]
 
@@ -114,9 +120,9 @@ def U_matrix_real(irreps_in, irreps_out, correlation: int, dtype=torch.float64):
 @functools.lru_cache(maxsize=None)
 def _U_matrix_real_cached(irreps_in: str, irreps_out: str, correlation: int):
     dtype = torch.float64
-    assert correlation <= 3
     irreps_out = Irreps(irreps_out)
-    wigners = _wigner_nj([Irreps(irreps_in)] * correlation, dtype)
+    filt = _FILTER_MID_C4 if correlation == 4 else None
+    wigners = _wigner_nj([Irreps(irreps_in)] * correlation, dtype, filt)
     current_ir = wigners[0][0]
     out, stack, last_ir = [], None, None
     for ir, _, base in wigners:
