@@ -97,13 +97,14 @@ def params_equal_across_ranks(params) -> bool:
     return bool(torch.equal(hi, lo))
 
 
-def make_params(layers: int, max_edge_radius: float, lmax: int = 4, storage: str = "float32"):
+def make_params(layers: int, max_edge_radius: float, lmax: int = 4, storage: str = "float32",
+                correlation: int = 3):
     from argparse import Namespace
     hid = "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
     ro = "+".join(f"16x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
     return Namespace(lmax=lmax, hidden_irreps=hid, readout_irreps=ro, num_edge_bases=6,
                      interaction_reduction="sum", interaction_bias=True, agg_norm_const=4.0,
-                     inter_MLP_dim=64, inter_MLP_layers=3, correlation=3, global_reduction="mean",
+                     inter_MLP_dim=64, inter_MLP_layers=3, correlation=correlation, global_reduction="mean",
                      message_passes=layers, positive_function="matrix_power_2",
                      max_edge_radius=max_edge_radius, lr=1e-3, beta1=0.9, epsilon=1e-8,
                      amsgrad=True, weight_decay=1e-8, storage_dtype=storage)
@@ -195,7 +196,7 @@ def _time_cpu_steps(step, budget_s: float, warmup: int, min_steps: int, max_step
 
 
 def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax: int = 4,
-                 full: bool = False):
+                 full: bool = False, correlation: int = 3):
     """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
     scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
     shape: fwd + loss + bwd on all the host cores this job has.  ``full``: BASELINE.md
@@ -210,7 +211,7 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax:
     ds = SyntheticLattices(1, n_nodes, n_edges, 1234)
     b = collate([ds[0]])
     torch.manual_seed(0)
-    m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius, lmax))
+    m = om.EnergyEquivGNN(make_params(layers, ds.max_edge_radius, lmax, correlation=correlation))
 
     def step():
         m.zero_grad(set_to_none=True)
@@ -369,6 +370,8 @@ def main():
     ap.add_argument("--edges", type=int, default=4096)
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--lmax", type=int, default=4)
+    ap.add_argument("--correlation", type=int, default=3, choices=[1, 2, 3, 4],
+                    help="symmetric-contraction correlation (4: the table-driven kernels, lmax <= 3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--cpu-full", action="store_true",
@@ -422,7 +425,7 @@ def main():
     rmax = torch.tensor([max(float(d.edge_attr.max()) for d in mine)], device=dev)
     if world > 1:
         dist.all_reduce(rmax, op=dist.ReduceOp.MAX)
-    params = make_params(args.layers, float(rmax.item()), args.lmax, args.storage)
+    params = make_params(args.layers, float(rmax.item()), args.lmax, args.storage, args.correlation)
     torch.manual_seed(0)
     model = EnergyEquivGNN(params).to(dev)
     # AdamW(amsgrad) as the reference configures it (scripts/train_utils.py:39-43); the fused
@@ -495,7 +498,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax,
-                               full=args.cpu_full)
+                               full=args.cpu_full, correlation=args.correlation)
         value = world * args.batch * args.steps / dt
         out = {
             "metric": ("lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU"
@@ -509,12 +512,13 @@ def main():
             "dtype": "f32" if args.storage == "float32" else "f32 (bf16 storage of w / grad_w / gxe)",
             "data": "synthetic periodic lattices (SURVEY 8d generator), random-init weights",
             "config": {"workload": f"EnergyEquivGNN {args.layers}-layer lmax{args.lmax} "
-                                   f"({args.storage} edge storage), "
+                                   + (f"correlation {args.correlation} " if args.correlation != 3 else "")
+                                   + f"({args.storage} edge storage), "
                                    f"{args.batch} graphs/GPU x {args.nodes} nodes/{args.edges} edges, "
                                    "fwd+loss+bwd+allreduce+clip+AdamW",
                        "global_batch": args.batch * world, "nodes_per_graph": args.nodes,
                        "edges_per_graph": args.edges, "layers": args.layers,
-                       "node_order": args.node_order,
+                       "correlation": args.correlation, "node_order": args.node_order,
                        "parallelism": f"graph-sharded dp{world}"},
             "backend": backend, "rehearsal": backend == "gloo",
             "loss": round(float(loss.item()), 6),
