@@ -11,8 +11,9 @@
 // component q; desc.orow[q] .. orow[q+1] is q's term range.  Layouts as the generated kernels:
 // node rows of mul-major irreps blocks, component a of channel c at x[n*ldx + xb[a] + c*xs[a]].
 //
-// Forward and grad-x: one thread per (node, channel), its components in an LDS column (no
-// barrier: a thread reads only its own column); the term loop is wave-uniform (scalar loads of
+// Forward and grad-x: one thread per (node, channel), its components in an LDS column (no barrier:
+// a thread reads only its own column), grad-x's accumulators in registers indexed by the
+// wave-uniform table entries (s_set_gpr_idx); the term loops are wave-uniform (scalar loads of
 // the table and the channel's coefficients).  Coefficient gradient: as sc_bwd_coef, one
 // workgroup = one channel x EELG_SCG_CHUNK LDS-resident nodes, each wave sweeps 64-term batches
 // over the chunk with per-lane accumulators, reduced over the 64 lanes (eelg_lane_reduce64);
@@ -27,11 +28,13 @@
 
 __device__ __forceinline__ int scg_i(unsigned tm, int k) { return (int)((tm >> (8 * k)) & 0xffu); }
 
+// Forward: the thread's components in an LDS column (row D = the constant 1), four terms per
+// iteration with their table entries, coefficients and LDS reads independent.
 __global__ __launch_bounds__(SCG_T) void scg_fwd_kernel(eelg_scg_desc d, const unsigned* __restrict__ terms,
                                                        const float* __restrict__ x, int ldx,
                                                        const float* __restrict__ coef, int ldc, int n_nodes,
                                                        float* __restrict__ out, int ldo) {
-  __shared__ float sx[(EELG_SCG_MAXD + 1) * SCG_T];
+  extern __shared__ float sx[];   // (D + 1) rows of SCG_T
   const int c = blockIdx.y, tid = threadIdx.x;
   const int n = blockIdx.x * SCG_T + tid;
   const bool ok = n < n_nodes;
@@ -41,60 +44,74 @@ __global__ __launch_bounds__(SCG_T) void scg_fwd_kernel(eelg_scg_desc d, const u
   const float* __restrict__ cr = coef + (size_t)c * ldc;
   const float* __restrict__ col = sx + tid;
   for (int q = 0; q < d.Dout; ++q) {
-    float acc = 0.0f;
-    for (int t = d.orow[q]; t < d.orow[q + 1]; ++t) {
-      const unsigned tm = terms[t];
-      const float v = col[scg_i(tm, 0) * SCG_T] * col[scg_i(tm, 1) * SCG_T] *
-                      col[scg_i(tm, 2) * SCG_T] * col[scg_i(tm, 3) * SCG_T];
-      acc = fmaf(cr[t], v, acc);
+    float acc = 0.0f, acc2 = 0.0f;
+    int t = d.orow[q];
+    const int te = d.orow[q + 1];
+    for (; t + 4 <= te; t += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned tm = terms[t + u];
+        v[u] = (col[scg_i(tm, 0) * SCG_T] * col[scg_i(tm, 1) * SCG_T]) *
+               (col[scg_i(tm, 2) * SCG_T] * col[scg_i(tm, 3) * SCG_T]);
+      }
+      acc = fmaf(cr[t], v[0], acc);
+      acc2 = fmaf(cr[t + 1], v[1], acc2);
+      acc = fmaf(cr[t + 2], v[2], acc);
+      acc2 = fmaf(cr[t + 3], v[3], acc2);
     }
-    if (ok) out[(size_t)n * ldo + d.ob[q] + c * d.os[q]] = acc;
+    for (; t < te; ++t) {
+      const unsigned tm = terms[t];
+      acc = fmaf(cr[t], (col[scg_i(tm, 0) * SCG_T] * col[scg_i(tm, 1) * SCG_T]) *
+                            (col[scg_i(tm, 2) * SCG_T] * col[scg_i(tm, 3) * SCG_T]), acc);
+    }
+    if (ok) out[(size_t)n * ldo + d.ob[q] + c * d.os[q]] = acc + acc2;
   }
 }
 
 // grad_x[a] = sum_t coef_t g_q(t) d(x_i0 x_i1 x_i2 x_i3)/dx_a: each factor slot k adds the
 // product of the other three to slot i_k's accumulator (a repeated index collects one
-// contribution per occurrence, the product rule).  The accumulators are the thread's own LDS
-// column (row D, the constant, collects and is dropped).
+// contribution per occurrence, the product rule).  The components are read from the thread's LDS
+// column; the accumulators live in registers indexed by the wave-uniform table entries
+// (s_set_gpr_idx; slot D, the constant, collects and is dropped), so the updates form no LDS
+// read-modify-write chains.
+template <int DM>
 __global__ __launch_bounds__(SCG_T) void scg_bwd_x_kernel(eelg_scg_desc d, const unsigned* __restrict__ terms,
                                                          const float* __restrict__ x, int ldx,
                                                          const float* __restrict__ coef, int ldc,
                                                          const float* __restrict__ gout, int ldg, int n_nodes,
                                                          float* __restrict__ gx) {
-  __shared__ float sx[(EELG_SCG_MAXD + 1) * SCG_T];
-  __shared__ float sg[(EELG_SCG_MAXD + 1) * SCG_T];
-  const int c = blockIdx.y, tid = threadIdx.x;
-  const int n = blockIdx.x * SCG_T + tid;
+  const int c = blockIdx.y;
+  const int n = blockIdx.x * SCG_T + threadIdx.x;
   const bool ok = n < n_nodes;
-  const size_t row = (size_t)(ok ? n : 0) * ldx;
-  for (int a = 0; a < d.D; ++a) {
-    sx[a * SCG_T + tid] = ok ? x[row + d.xb[a] + c * d.xs[a]] : 0.0f;
-    sg[a * SCG_T + tid] = 0.0f;
-  }
-  sx[d.D * SCG_T + tid] = 1.0f;
-  sg[d.D * SCG_T + tid] = 0.0f;
+  const size_t row = (size_t)(ok ? n : 0) * ldx, grow = (size_t)(ok ? n : 0) * ldg;
+  extern __shared__ float sx[];   // (D + 1) rows of SCG_T: the components, row D = 1
+  float gr[DM];
+#pragma unroll
+  for (int a = 0; a < DM; ++a) gr[a] = 0.0f;
+  for (int a = 0; a < d.D; ++a) sx[a * SCG_T + threadIdx.x] = ok ? x[row + d.xb[a] + c * d.xs[a]] : 0.0f;
+  sx[d.D * SCG_T + threadIdx.x] = 1.0f;
+  const float* __restrict__ col = sx + threadIdx.x;
   const float* __restrict__ cr = coef + (size_t)c * ldc;
-  const float* __restrict__ col = sx + tid;
-  float* __restrict__ gcol = sg + tid;
-  const size_t grow = (size_t)(ok ? n : 0) * ldg;
   for (int q = 0; q < d.Dout; ++q) {
     if (d.orow[q] == d.orow[q + 1]) continue;   // uniform
     const float go = ok ? gout[grow + d.ob[q] + c * d.os[q]] : 0.0f;
+#pragma unroll 4
     for (int t = d.orow[q]; t < d.orow[q + 1]; ++t) {
       const unsigned tm = terms[t];
-      const int i0 = scg_i(tm, 0) * SCG_T, i1 = scg_i(tm, 1) * SCG_T, i2 = scg_i(tm, 2) * SCG_T,
-                i3 = scg_i(tm, 3) * SCG_T;
-      const float x0 = col[i0], x1 = col[i1], x2 = col[i2], x3 = col[i3];
+      const int i0 = scg_i(tm, 0), i1 = scg_i(tm, 1), i2 = scg_i(tm, 2), i3 = scg_i(tm, 3);
+      const float x0 = col[i0 * SCG_T], x1 = col[i1 * SCG_T], x2 = col[i2 * SCG_T], x3 = col[i3 * SCG_T];
       const float cg = cr[t] * go;
       const float p01 = x0 * x1, p23 = x2 * x3;
-      gcol[i0] = fmaf(cg * x1, p23, gcol[i0]);
-      gcol[i1] = fmaf(cg * x0, p23, gcol[i1]);
-      gcol[i2] = fmaf(cg * x3, p01, gcol[i2]);
-      gcol[i3] = fmaf(cg * x2, p01, gcol[i3]);
+      gr[i0] = fmaf(cg * x1, p23, gr[i0]);
+      gr[i1] = fmaf(cg * x0, p23, gr[i1]);
+      gr[i2] = fmaf(cg * x3, p01, gr[i2]);
+      gr[i3] = fmaf(cg * x2, p01, gr[i3]);
     }
   }
-  if (ok)
-    for (int a = 0; a < d.D; ++a) gx[row + d.xb[a] + c * d.xs[a]] = gcol[a * SCG_T];
+#pragma unroll
+  for (int a = 0; a < DM; ++a)
+    if (ok && a < d.D) gx[row + d.xb[a] + c * d.xs[a]] = gr[a];
 }
 
 // partial[ch, c, t] = sum over chunk ch's nodes of g_{out[t]} * x_i0 x_i1 x_i2 x_i3.  LDS:
@@ -131,12 +148,17 @@ __global__ __launch_bounds__(SCG_T) void scg_bwd_coef_kernel(eelg_scg_desc d, co
     for (int s = 0; s < CH / 64; ++s) {
       const float* __restrict__ xc = sx + s * 64 + lane;
       const float* __restrict__ gc = sg + s * 64 + lane;
+      // the batch's table is re-read (scalar cache) per sub-tile: hoisted out of the loop, its
+      // 128 words would not fit the SGPRs and spill into VGPR lanes
+      const unsigned* tp = terms + t0;
+      const int* op = tout + t0;
+      asm volatile("" : "+s"(tp), "+s"(op));
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const unsigned tm = terms[t0 + i];
-        const float v = xc[scg_i(tm, 0) * CH] * xc[scg_i(tm, 1) * CH] * xc[scg_i(tm, 2) * CH] *
-                        xc[scg_i(tm, 3) * CH];
-        acc[i] = fmaf(gc[tout[t0 + i] * CH], v, acc[i]);
+        const unsigned tm = tp[i];
+        const float v = (xc[scg_i(tm, 0) * CH] * xc[scg_i(tm, 1) * CH]) *
+                        (xc[scg_i(tm, 2) * CH] * xc[scg_i(tm, 3) * CH]);
+        acc[i] = fmaf(gc[op[i] * CH], v, acc[i]);
       }
     }
     eelg_lane_reduce64(acc);
@@ -166,8 +188,8 @@ int eelg_scg_fwd(const eelg_scg_desc* d, const unsigned* terms, const float* x, 
   if (n_nodes < 0) return eelg_fail(-2, "scg_fwd: negative node count");
   if (n_nodes == 0) return 0;
   const dim3 grid((n_nodes + SCG_T - 1) / SCG_T, d->mul);
-  hipLaunchKernelGGL(scg_fwd_kernel, grid, dim3(SCG_T), 0, (hipStream_t)stream, *d, terms, x, ldx, coef, ldc,
-                     n_nodes, out, ldo);
+  hipLaunchKernelGGL(scg_fwd_kernel, grid, dim3(SCG_T), (d->D + 1) * SCG_T * sizeof(float), (hipStream_t)stream,
+                     *d, terms, x, ldx, coef, ldc, n_nodes, out, ldo);
   return eelg_check_launch("scg_fwd");
 }
 
@@ -177,8 +199,12 @@ int eelg_scg_bwd_x(const eelg_scg_desc* d, const unsigned* terms, const float* x
   if (n_nodes < 0) return eelg_fail(-2, "scg_bwd_x: negative node count");
   if (n_nodes == 0) return 0;
   const dim3 grid((n_nodes + SCG_T - 1) / SCG_T, d->mul);
-  hipLaunchKernelGGL(scg_bwd_x_kernel, grid, dim3(SCG_T), 0, (hipStream_t)stream, *d, terms, x, ldx, coef, ldc,
-                     grad_out, ldg, n_nodes, grad_x);
+  if (d->D <= 16)
+    hipLaunchKernelGGL(scg_bwd_x_kernel<17>, grid, dim3(SCG_T), (d->D + 1) * SCG_T * sizeof(float),
+                       (hipStream_t)stream, *d, terms, x, ldx, coef, ldc, grad_out, ldg, n_nodes, grad_x);
+  else
+    hipLaunchKernelGGL(scg_bwd_x_kernel<EELG_SCG_MAXD + 1>, grid, dim3(SCG_T), (d->D + 1) * SCG_T * sizeof(float),
+                       (hipStream_t)stream, *d, terms, x, ldx, coef, ldc, grad_out, ldg, n_nodes, grad_x);
   return eelg_check_launch("scg_bwd_x");
 }
 

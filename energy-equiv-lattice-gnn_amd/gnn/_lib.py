@@ -114,7 +114,7 @@ class GateDesc(ctypes.Structure):
 
 
 SCG_MAXD = 25            # include/eelg.h EELG_SCG_MAXD / EELG_SCG_CHUNK
-SCG_CHUNK = 512
+SCG_CHUNK = 256
 
 
 class ScgDesc(ctypes.Structure):

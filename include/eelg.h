@@ -254,7 +254,7 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes,
  * partials [ceil(n_nodes / EELG_SCG_CHUNK), mul, ldc] (term_out[t]: output of term t; padding
  * terms t >= nterms need indices D and output Dout: they produce 0); the caller sums them. */
 #define EELG_SCG_MAXD 25
-#define EELG_SCG_CHUNK 512
+#define EELG_SCG_CHUNK 256
 typedef struct {
   int D, Dout, mul, nterms;
   int xb[EELG_SCG_MAXD], xs[EELG_SCG_MAXD];
