@@ -168,9 +168,48 @@ class Linear(torch.nn.Linear):
         return y.view(*shape[:-1], self.out_features)
 
 
+# the K <= 8 node-embedding linear as addcmul + sum_rows (1) or autograd's broadcast form (0)
+SMALLIN_FUSED = os.environ.get("EELG_SMALLIN_FUSED", "1") != "0"
+
+
+class _SmallIn(torch.autograd.Function):
+    """``x @ W^T + b`` for K <= 8 inputs that need no gradient (node attributes / positions):
+    forward one ``addcmul`` per input column onto the bias, backward the weight and bias
+    gradients as fixed-order column sums on ``ops.sum_rows`` (one [N, K * n_out] product for the
+    weight) instead of autograd's broadcast multiplies and ``torch.sum`` reductions."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        n, k = x.shape
+        if bias is not None:
+            out = torch.addcmul(bias, x[:, :1], weight[:, 0])
+        else:
+            out = x[:, :1] * weight[:, 0]
+        for c in range(1, k):
+            out.addcmul_(x[:, c: c + 1], weight[:, c])
+        ctx.save_for_backward(x)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        gy = ops._f32(gy).contiguous()
+        n, k = x.shape
+        gw = gb = None
+        if ctx.needs_input_grad[1]:
+            prod = (x.float()[:, :, None] * gy[:, None, :]).reshape(n, -1)     # [N, K * n_out]
+            gw = ops.sum_rows(prod).view(k, -1).t()
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = ops.sum_rows(gy)
+        return None, gw, gb
+
+
 def small_in_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
     """``x @ W^T + b`` for a handful of inputs (the node embeddings, K = 1 or 3) as broadcast
     multiply-adds: a K-term outer product is elementwise work, not a GEMM."""
+    if SMALLIN_FUSED and x.is_cuda and not x.requires_grad and x.dtype == torch.float32 and x.shape[1] <= 8:
+        return _SmallIn.apply(x, weight, bias)
     out = bias.expand(x.shape[0], -1) if bias is not None else None
     for c in range(x.shape[1]):
         term = x[:, c: c + 1] * weight[:, c]

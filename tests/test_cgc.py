@@ -240,3 +240,29 @@ def test_cgc_fused_residual_matches_explicit_add(d, reduction):
     assert torch.equal(a[0], r[0])
     for u, v in zip(a[1:], r[1:]):
         assert _rel(u, v) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n_out,bias,rows", [(1, 128, True, 5000), (3, 64, True, 777), (3, 32, False, 300)])
+def test_small_in_linear_matches_fp64(k, n_out, bias, rows):
+    """The node embeddings' K <= 8 linear (dense.small_in_linear: addcmul forward, weight and bias
+    gradients as sum_rows column sums) against an fp64 torch linear: output, weight and bias
+    gradients within 2e-6 of their largest entry."""
+    from gnn import dense
+    torch.manual_seed(0)
+    lin = dense.SmallInLinear(k, n_out, bias=bias).cuda()
+    x = torch.randn(rows, k, device="cuda")
+    g = torch.randn(rows, n_out, device="cuda")
+    y = lin(x)
+    y.backward(g)
+    w64 = lin.weight.detach().double().requires_grad_(True)
+    b64 = lin.bias.detach().double().requires_grad_(True) if bias else None
+    y64 = torch.nn.functional.linear(x.double(), w64, b64)
+    y64.backward(g.double())
+
+    def rel(a, b):
+        return float((a.double() - b).abs().max() / b.abs().max())
+    assert rel(y, y64) < 2e-6
+    assert rel(lin.weight.grad, w64.grad) < 2e-6
+    if bias:
+        assert rel(lin.bias.grad, b64.grad) < 2e-6
