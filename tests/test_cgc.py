@@ -261,7 +261,7 @@ def test_small_in_linear_matches_fp64(k, n_out, bias, rows):
     y64.backward(g.double())
 
     def rel(a, b):
-        return float((a.double() - b).abs().max() / b.abs().max())
+        return float((a.detach().double() - b.detach()).abs().max() / b.detach().abs().max())
     assert rel(y, y64) < 2e-6
     assert rel(lin.weight.grad, w64.grad) < 2e-6
     if bias:
