@@ -27,6 +27,8 @@ from .blocks import EdgeIndex, as_csr, mat_square
 # Same box (r06n): 32,425 vs 31,940 / 31,753 graphs/s, and the aggregation kernel's roofline
 # fraction (its residual read counted) 0.436 vs 0.422 / 0.424
 CGC_FUSED_RES = os.environ.get("EELG_CGC_FUSED_RES", "1") != "0"
+# every layer's edge factor in one batched pass (1) or per layer (0)
+CGC_EA_BATCH = os.environ.get("EELG_CGC_EA_BATCH", "1") != "0"
 
 # Mandel 6x6 from the 21 upper-triangular outputs (cgc_modified.py:28-33)
 INDS_VAL = [[0, 1, 2, 3, 4, 5],
@@ -262,10 +264,22 @@ class _CGCBase(torch.nn.Module):
         ef = torch.cat([e5, torch.ones_like(e5[:, :1]), torch.zeros_like(e5[:, :2])], dim=1).contiguous()
         return csr, self.node_ft_embedding(node_in), ef
 
-    def _layer(self, i, h, csr, ef, residual: bool = False):
-        """layer i (h + layer_i(h) when ``residual``)"""
+    def _edge_factors(self):
+        """every layer's ``ea`` [8, 2D] (``_edge_factor``) in one batched pass: the edge embedding
+        is shared, so the products and sums of the layers (and their backward) run as one set of
+        launches instead of one per layer"""
+        we = torch.stack([layer.edge_block() for layer in self.cgc_layers])   # [L, 2D, D]
+        w5, b5 = self.edge_ft_embedding.weight, self.edge_ft_embedding.bias    # [D, 5], [D]
+        a = (w5.t()[None, :, None, :] * we[:, None, :, :]).sum(-1)           # [L, 5, 2D]
+        c = (we * b5[None, None, :]).sum(-1)                                 # [L, 2D]
+        pad = torch.zeros(we.shape[0], 2, we.shape[1], device=we.device, dtype=we.dtype)
+        return torch.cat([a, c[:, None], pad], dim=1)                        # [L, 8, 2D]
+
+    def _layer(self, i, h, csr, ef, residual: bool = False, ea=None):
+        """layer i (h + layer_i(h) when ``residual``); ``ea``: its edge factor if precomputed"""
         layer = self.cgc_layers[i]
-        ea = _edge_factor(self.edge_ft_embedding, layer.edge_block())
+        if ea is None:
+            ea = _edge_factor(self.edge_ft_embedding, layer.edge_block())
         if residual and not CGC_FUSED_RES:
             return h + layer.forward_factored(h, csr, ef, ea)
         return layer.forward_factored(h, csr, ef, ea, residual)
@@ -282,9 +296,10 @@ class CrystGraphConv(_CGCBase):
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         csr, h, ef = self._encode(batch, batch.node_attrs)
-        h = self._layer(0, h, csr, ef)
+        ea = self._edge_factors() if CGC_EA_BATCH else [None] * len(self.cgc_layers)
+        h = self._layer(0, h, csr, ef, ea=ea[0])
         for i in range(1, len(self.cgc_layers)):
-            h = self._layer(i, h, csr, ef, residual=True)   # h + layer_i(h)
+            h = self._layer(i, h, csr, ef, residual=True, ea=ea[i])   # h + layer_i(h)
         a = self.mlp(self._pool(h, batch))[:, self.inds_val]
         if self.params.positive == "square":
             return {"stiffness": mat_square(a)}
@@ -300,6 +315,7 @@ class CrystGraphConvVanilla(_CGCBase):
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         csr, h, ef = self._encode(batch, batch.positions)
+        ea = self._edge_factors() if CGC_EA_BATCH else [None] * len(self.cgc_layers)
         for i in range(len(self.cgc_layers)):
-            h = self._layer(i, h, csr, ef, residual=True)   # h + layer_i(h)
+            h = self._layer(i, h, csr, ef, residual=True, ea=ea[i])   # h + layer_i(h)
         return {"stiffness": self.mlp(self._pool(h, batch))}
