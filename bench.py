@@ -179,16 +179,24 @@ def host_cpu() -> dict:
             "isa": torch.backends.cpu.get_cpu_capability()}
 
 
-def _time_cpu_steps(step, budget_s: float, warmup: int, min_steps: int, max_steps: int):
+def _time_cpu_steps(step, budget_s: float, warmup: int, min_steps: int, max_steps: int,
+                    progress: str = ""):
     """``warmup`` untimed steps, then timed steps until ``min_steps`` are done and the budget is
-    spent, or ``max_steps`` are done (3 warm-up + >= 10 timed)."""
-    for _ in range(warmup):
+    spent, or ``max_steps`` are done (3 warm-up + >= 10 timed).
+    ``progress``: a label; one line per step goes to stderr (a long CPU leg is not silent)."""
+    for i in range(warmup):
+        t0 = time.perf_counter()
         step()
+        if progress:
+            print(f"{progress}: warm-up {i + 1}/{warmup} {time.perf_counter() - t0:.2f} s",
+                  file=sys.stderr, flush=True)
     times, t_start = [], time.perf_counter()
     while len(times) < max_steps:
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
+        if progress:
+            print(f"{progress}: timed {len(times)} {times[-1]:.2f} s", file=sys.stderr, flush=True)
         if len(times) >= min_steps and time.perf_counter() - t_start > budget_s:
             break
     times.sort()
@@ -196,12 +204,13 @@ def _time_cpu_steps(step, budget_s: float, warmup: int, min_steps: int, max_step
 
 
 def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax: int = 4,
-                 full: bool = False, correlation: int = 3):
+                 full: bool = True, correlation: int = 3):
     """The oracle (pure-PyTorch CPU restatement of the reference, dense per-path TP,
     scatter_add_, opt_einsum-order symmetric contraction) on ONE graph of the same
-    shape: fwd + loss + bwd on all the host cores this job has.  ``full``: BASELINE.md
-    section 2's protocol (3 warm-up + 10 timed steps, ~4 min); default: 1 warm-up and
-    timed steps within ``budget_s`` (at least 1), so that the default bench run stays short."""
+    shape: fwd + loss + bwd on all the host cores this job has.  ``full`` (default):
+    BASELINE.md section 2's protocol, 3 warm-up + 10 timed steps (about 3.5 min on 16 EPYC
+    threads); ``full=False`` (``bench.py --cpu-quick``): 1 warm-up and timed steps within
+    ``budget_s`` (at least 1)."""
     import oracle.model as om
     from oracle.train import stiffness_loss
     from gnn.data import collate
@@ -218,7 +227,7 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax:
         stiffness_loss(m(b)["stiffness"], b.stiffness).backward()
 
     warm, lo, hi = (3, 10, 10) if full else (1, 1, 10)
-    t = _time_cpu_steps(step, budget_s, warm, lo, hi)
+    t = _time_cpu_steps(step, budget_s, warm, lo, hi, progress="cpu_baseline")
     med = statistics.median(t)
     pct = lambda q: t[min(len(t) - 1, int(q * (len(t) - 1) + 0.5))]  # noqa: E731
     return {"value": round(1.0 / med, 4), "unit": "lattice-graphs/s", "cores": host["threads"],
@@ -226,8 +235,31 @@ def cpu_baseline(n_nodes: int, n_edges: int, layers: int, budget_s: float, lmax:
             "sample": f"oracle fp32 fwd+loss+bwd, 1 graph x {n_nodes} nodes/{n_edges} edges, "
                       f"{layers} layers lmax {lmax}; {warm} warm-up + {len(t)} timed step(s): median "
                       f"{med:.2f} s, p10 {pct(0.1):.2f} s, p90 {pct(0.9):.2f} s" +
-                      ("" if full else f" (budget {budget_s:.0f} s; BASELINE.md section 2's 3 + 10 "
-                                        "steps: bench.py --cpu-full)")}
+                      (" (BASELINE.md section 2 protocol)" if full else
+                       f" (budget {budget_s:.0f} s, bench.py --cpu-quick; BASELINE.md section 2's "
+                       "3 + 10 steps are the default)")}
+
+
+def inline_kernel_times(step, steps: int) -> dict:
+    """Per-op HIP-event times (ops.TIMER) over ``steps`` training steps run in line: every kernel
+    on the main stream in EELG_OVERLAP=0's order (one untimed step first).  The side-stream overlap
+    is switched back on afterwards.  Every rank runs it (the step holds the all-reduce)."""
+    from gnn import ops
+    saved = ops.OVERLAP
+    ops.OVERLAP = False
+    try:
+        step()
+        torch.cuda.synchronize()
+        ops.TIMER.enabled = True
+        ops.TIMER.records.clear()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ops.TIMER.enabled = False
+        return ops.TIMER.summary()
+    finally:
+        ops.TIMER.enabled = False
+        ops.OVERLAP = saved
 
 
 def cgc_fwd_bytes(n: int, e: int, d: int, residual: bool = False) -> int:
@@ -375,8 +407,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--cpu-full", action="store_true",
-                    help="CPU baseline with BASELINE.md section 2's 3 warm-up + 10 timed steps")
+                    help="(default) CPU baseline with BASELINE.md section 2's 3 warm-up + 10 timed steps")
+    ap.add_argument("--cpu-quick", action="store_true",
+                    help="CPU baseline with 1 warm-up + timed steps within --cpu-budget (at least 1)")
     ap.add_argument("--kernel-summary", action="store_true", help="print per-kernel timings to stderr")
+    ap.add_argument("--inline-steps", type=int, default=5,
+                    help="in-line steps after the timed region whose tp_fwd launch time gives the "
+                         "roofline (0: the overlapped timed region's own figure)")
     ap.add_argument("--model", default="egnn", choices=["egnn", "cgc_modified", "cgc_vanilla"],
                     help="egnn = the headline EnergyEquivGNN; cgc_* = BASELINE config 4 benchmark models")
     ap.add_argument("--optimizer", default="fused", choices=["fused", "foreach"],
@@ -470,6 +507,11 @@ def main():
         dt = float(t.item())
     ksum = ops.TIMER.summary()
     same = params_equal_across_ranks(plist) if (world > 1 and args.check_params) else None
+    # the roofline kernel's launch time in the in-line step (every kernel on the main stream,
+    # EELG_OVERLAP=0's order), after the timed region: the figure a rocprofv3 kernel trace of
+    # this command reproduces (profiles/r08a_frac_probe.md); the overlapped timed region's own
+    # HIP-event figure is reported beside it
+    ksum_inl = inline_kernel_times(step, args.inline_steps) if args.inline_steps > 0 else {}
 
     if rank == 0:
         n_tot = args.batch * args.nodes
@@ -481,7 +523,12 @@ def main():
         if key in ksum:
             byts = tp_fwd_bytes(n_tot, e_tot, info["din"], info["wn"], info["dmid"], info["nsh"],
                                 2 if args.storage == "bfloat16" else 4)
-            ms = ksum[key]["mean_ms"]
+            ovl = {"mean_ms": round(ksum[key]["mean_ms"], 4), "launches": ksum[key]["count"],
+                   "frac": round(byts / (ksum[key]["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                   "timing": "HIP events on the launch stream over the timed region (side-stream "
+                             "overlap on, the step the value is measured on)"}
+            src = ksum_inl if key in ksum_inl else ksum
+            ms = src[key]["mean_ms"]
             ach = byts / (ms * 1e-3) / 1e9
             # the generated kernel's name (the bf16-storage form carries the _bw suffix)
             kname = f"tp_fwd_tpB_l{args.lmax}" + ("_bw" if args.storage == "bfloat16" else "")
@@ -489,7 +536,12 @@ def main():
                     "frac": round(ach / HBM_PEAK_GBPS, 4),
                     "traffic": None, "traffic_detail": pmc_traffic(kname, args),
                     "kernel": f"{kname} (fused gather+TP+segmented sum)",
-                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": ksum[key]["count"]}
+                    "bytes_per_launch": byts, "mean_ms": round(ms, 4), "launches": src[key]["count"],
+                    "timing": ("HIP events on the launch stream, in-line step (EELG_OVERLAP=0 order, "
+                               f"{args.inline_steps} steps after the timed region): agrees with the "
+                               "rocprofv3 kernel trace of this command, profiles/r08a_frac_probe.md"
+                               if src is ksum_inl else ovl["timing"]),
+                    "overlapped": ovl}
             if roof["traffic_detail"]:
                 roof["traffic"] = roof["traffic_detail"]["bytes"]      # HBM bytes per launch (PMC)
                 # measured HBM bytes over the SURVEY 8d algorithmic bytes (x is gathered once per
@@ -498,7 +550,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.nodes, args.edges, args.layers, args.cpu_budget, args.lmax,
-                               full=args.cpu_full, correlation=args.correlation)
+                               full=not args.cpu_quick, correlation=args.correlation)
         value = world * args.batch * args.steps / dt
         out = {
             "metric": ("lattice-graphs/s (fwd+bwd), 4-layer EnergyEquivGNN, ~1k nodes/~4k edges, 1/2/4/8 GPU"

@@ -559,13 +559,21 @@ int eelg_tp_fwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
   return check_launch("tp_fwd_bf16");
 }
 
+// tp_bwd: 8 half-waves x beph edges per block; with bxcd the grid is 1-D, the edge blocks rounded
+// up to a multiple of 8 so that XCD k takes one contiguous range of them (gen_kernels.py)
+static dim3 tp_bwd_grid(const eelg_tp_cfg& c, int n_edges) {
+  const int nb = (n_edges + 8 * c.beph - 1) / (8 * c.beph);
+  if (!c.bxcd) return dim3(nb, c.nbgroups);
+  return dim3(((nb + 7) / 8) * 8 * c.nbgroups);
+}
+
 int eelg_tp_bwd_sorted(int cfg, const float* x, const float* sh, const float* w, const int* sender,
                        const int* receiver, const int* spos, int n_edges, const float* grad_agg,
                        float inv_norm, float* grad_w, float* gxe, void* stream) {
   const eelg_tp_cfg* c = tp_cfg(cfg);
   if (!c) return -1;
   if (n_edges <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd, tp_bwd_grid(*c, n_edges), dim3(256), 0,
                      (hipStream_t)stream, x, sh, w, sender, receiver, n_edges, grad_agg, inv_norm,
                      grad_w, gxe, spos);
   return check_launch("tp_bwd");
@@ -586,7 +594,7 @@ int eelg_tp_bwd_sorted_bf16(int cfg, const float* x, const float* sh, const void
   if (!c) return -1;
   if (!c->bwd_bf) return fail(-2, "tp_bwd_bf16: bf16 storage is generated for mul 32 only (config %s)", c->name);
   if (n_edges <= 0) return 0;
-  hipLaunchKernelGGL(c->bwd_bf, dim3((n_edges + 8 * c->beph - 1) / (8 * c->beph), c->nbgroups), dim3(256), 0,
+  hipLaunchKernelGGL(c->bwd_bf, tp_bwd_grid(*c, n_edges), dim3(256), 0,
                      (hipStream_t)stream, x, sh, static_cast<const unsigned short*>(w), sender,
                      receiver, n_edges, grad_agg, inv_norm, static_cast<unsigned short*>(grad_w),
                      static_cast<unsigned short*>(gxe), spos);
@@ -684,7 +692,7 @@ static int cgc_launch_fwd(const float* ps, const float* pr, const float* ep, con
   if (D <= 0) return fail(-2, "cgc_fwd: D must be positive");
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_fwd: D = %d > %d not built", D, EELG_CGC_MAXD);
-  const dim3 g((n_nodes + 3) / 4);
+  const dim3 g(cgc_grid((n_nodes + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define CGCF(C, E) hipLaunchKernelGGL((cgc_fwd_kernel<C, E>), g, dim3(256), 0, st, ps, pr, ep, ef, ea, \
                                       sender, rowptr, row_scale, n_nodes, D, agg, res)
@@ -702,7 +710,7 @@ static int cgc_launch_bwd(const float* ps, const float* pr, const float* ep, con
   if (D <= 0) return fail(-2, "cgc_bwd: D must be positive");
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_bwd: D = %d > %d not built", D, EELG_CGC_MAXD);
-  const dim3 g((n_nodes + 3) / 4);
+  const dim3 g(cgc_grid((n_nodes + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define CGCB(C, E) hipLaunchKernelGGL((cgc_bwd_kernel<C, E>), g, dim3(256), 0, st, ps, pr, ep, ef, ea, \
                                       sender, rowptr, row_scale, n_nodes, D, grad_agg, dz, grad_pr)
@@ -749,7 +757,7 @@ static int cgc_launch_stream(bool bwd, const float* ps, const float* pr, const f
   if (n_nodes <= 0) return 0;
   if (D > EELG_CGC_MAXD) return fail(-2, "cgc_stream: D = %d > %d not built", D, EELG_CGC_MAXD);
   const int waves = (n_nodes + CGC_RPW - 1) / CGC_RPW;
-  const dim3 g((waves + 3) / 4);
+  const dim3 g(cgc_grid((waves + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define CGCS(C, B) hipLaunchKernelGGL((cgc_stream_kernel<C, B>), g, dim3(256), 0, st, ps, pr, ef, ea, \
                                       sender, receiver, rowptr, row_scale, n_nodes, D, agg, grad_agg, \
@@ -881,6 +889,24 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
   return check_launch("sc_cmajor");
 }
 
+// streaming coefficient gradient: the nodes are split into at most 4 ranges (one partial row
+// each) of whole chunks, so that 32 channels x 4 ranges x the term-group sets fill the chip
+// several times over without a workgroup per chunk
+static int sc_coef_range(const eelg_sc_cfg& c, int n_nodes) {
+  int nr = (n_nodes + 8191) / 8192;
+  nr = nr < 1 ? 1 : (nr > 4 ? 4 : nr);
+  const int rn = (n_nodes + nr - 1) / nr;
+  return (rn + c.nbc - 1) / c.nbc * c.nbc;
+}
+
+int eelg_sc_bwd_coef_parts(int cfg, int n_nodes, int mul) {
+  const eelg_sc_cfg* c = sc_get(cfg, mul);
+  if (!c) return -1;
+  if (n_nodes <= 0) return 0;
+  const int rn = c->bwd_coefs ? sc_coef_range(*c, n_nodes) : c->nbc;
+  return (n_nodes + rn - 1) / rn;
+}
+
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int mul, int chunk,
                      float* partial, void* stream) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
@@ -889,6 +915,14 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
     return fail(-2, "sc_bwd_coef: chunk must be the config's coefficient chunk %d (info[6]), got %d",
                 c->nbc, chunk);
   if (n_nodes <= 0) return 0;
+  if (c->bwd_coefs) {
+    // one workgroup per (channel x node range tile, term-group set); partial[range, channel, t]
+    const int rn = sc_coef_range(*c, n_nodes);
+    const int tiles = mul * ((n_nodes + rn - 1) / rn);
+    hipLaunchKernelGGL(c->bwd_coefs, dim3(((tiles + 7) / 8) * 8 * c->csets), dim3(1024), 0,
+                       (hipStream_t)stream, xt, gt, n_nodes, rn, partial);
+    return check_launch("sc_bwd_coefs");
+  }
   // one workgroup per (chunk of nbc LDS-resident nodes, channel)
   const int nch = (n_nodes + chunk - 1) / chunk;
   hipLaunchKernelGGL(c->bwd_coef, dim3(nch, mul), dim3(64 * c->wpb), 0, (hipStream_t)stream, xt, gt,

@@ -24,11 +24,17 @@
 #endif
 #if CGC_FAST_MATH
 // hardware exp2 / log2 / reciprocal (v_exp_f32, v_log_f32, v_rcp_f32: about 1 ulp each):
-// softplus(z) = max(z, 0) + log(1 + exp(-|z|)) never overflows and keeps torch's threshold
+// softplus(z) = max(z, 0) + log1p(exp(-|z|)) never overflows and keeps torch's threshold.
+// log1p(t) with the rounding of u = 1 + t corrected (log(u) * t / (u - 1); t itself once
+// u rounds to 1), so that softplus keeps its relative accuracy for negative z, where it is
+// about exp(z) (log(1 + t) alone loses ~0.3 % at z = -10 and is 0 below -16.6)
 __device__ __forceinline__ float cgc_softplus(float z) {
   if (z > 20.0f) return z;
   const float t = __builtin_amdgcn_exp2f(-fabsf(z) * 1.4426950408889634f);
-  return fmaxf(z, 0.0f) + __builtin_amdgcn_logf(1.0f + t) * 0.6931471805599453f;
+  const float u = 1.0f + t;
+  const float lp = u == 1.0f ? t
+      : __builtin_amdgcn_logf(u) * 0.6931471805599453f * t * __builtin_amdgcn_rcpf(u - 1.0f);
+  return fmaxf(z, 0.0f) + lp;
 }
 __device__ __forceinline__ float cgc_sigmoid(float z) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * 1.4426950408889634f));
@@ -37,6 +43,23 @@ __device__ __forceinline__ float cgc_sigmoid(float z) {
 __device__ __forceinline__ float cgc_softplus(float z) { return z > 20.0f ? z : log1pf(expf(z)); }
 __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + expf(-z)); }
 #endif
+
+// Block order (CGC_XCD, round 6): hardware block b runs on XCD b % 8.  With the grid padded to
+// a multiple of 8, logical block (b % 8) * (gridDim.x / 8) + b / 8 hands XCD k one contiguous
+// range of receivers, i.e. whole lattices in order, so a lattice's gathered Ps rows (1 KiB per
+// node at D = 128, 1 MiB per 1024-node lattice) are fetched into one L2 and re-read there by
+// the node's other out-edges, instead of being fetched by all eight L2s
+#ifndef CGC_XCD
+#define CGC_XCD 1
+#endif
+__device__ __forceinline__ int cgc_block() {
+#if CGC_XCD
+  return (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+#else
+  return blockIdx.x;
+#endif
+}
+static inline unsigned cgc_grid(unsigned blocks) { return CGC_XCD ? (blocks + 7) / 8 * 8 : blocks; }
 
 // Forward: a receiver's in-edges are taken CGC_EB at a time: their sender indices are
 // wave-uniform (one scalar load batch), and every lane issues the batch's gathers of Ps[s] and
@@ -92,7 +115,7 @@ __global__ __launch_bounds__(256) void cgc_fwd_kernel(
     const float* __restrict__ ef, const float* __restrict__ ea,
     const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, float* __restrict__ agg, const float* __restrict__ res) {
-  const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int node = __builtin_amdgcn_readfirstlane(cgc_block() * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (node >= n_nodes) return;
   const int beg = rowptr[node], end = rowptr[node + 1];
@@ -152,7 +175,7 @@ __global__ __launch_bounds__(256) void cgc_bwd_kernel(
     const float* __restrict__ ps, const float* __restrict__ pr, const float* __restrict__ ep,
     const float* __restrict__ ef, const float* __restrict__ ea, const int* __restrict__ sender, const int* __restrict__ rowptr, const float* __restrict__ row_scale,
     int n_nodes, int D, const float* __restrict__ gagg, float* __restrict__ dz, float* __restrict__ gr) {
-  const int node = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int node = __builtin_amdgcn_readfirstlane(cgc_block() * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (node >= n_nodes) return;
   const int beg = rowptr[node], end = rowptr[node + 1];
@@ -286,7 +309,11 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
     const int* __restrict__ rowptr, const float* __restrict__ row_scale, int n_nodes, int D,
     float* __restrict__ agg, const float* __restrict__ gagg, float* __restrict__ dz,
     float* __restrict__ gr, float* __restrict__ dea_part) {
-  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int bx = cgc_block();
+  // a padding block of the XCD-ordered grid (past the last receiver group) leaves before the
+  // workgroup reduction and writes no partial
+  if (bx >= ((n_nodes + CGC_RPW - 1) / CGC_RPW + 3) / 4) return;
+  const int wid = __builtin_amdgcn_readfirstlane(bx * 4 + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int r0 = wid * CGC_RPW;
   // a wave past the last receiver still takes part in the workgroup's reduction of the
@@ -403,7 +430,7 @@ __global__ __launch_bounds__(256) void cgc_stream_kernel(
         red[((w * CGC_EFN + i) * 2 + 1) * 64 * CPL + q * 64 + lane] = dam[i][q];
       }
     __syncthreads();
-    float* __restrict__ dst = dea_part + (size_t)blockIdx.x * CGC_EFN * D2;
+    float* __restrict__ dst = dea_part + (size_t)bx * CGC_EFN * D2;
     for (int t = threadIdx.x; t < CGC_EFN * 2 * 64 * CPL; t += 256) {
       const int i = t / (2 * 64 * CPL), rem = t - i * 2 * 64 * CPL;
       const int half = rem / (64 * CPL), c = rem - half * 64 * CPL;   // c = q * 64 + lane

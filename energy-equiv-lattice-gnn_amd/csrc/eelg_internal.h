@@ -40,6 +40,7 @@ struct eelg_tp_cfg {
   eelg_tp_bws_fn bws;        // sender-order backward (grad_x summed per sender in registers)
   eelg_tp_bws_bf_fn bws_bf;
   int ngroups_bf;            // path groups of the bf16-weight forward (its own accumulator cap)
+  int bxcd;                  // tp_bwd block placement (gen_kernels.TP_BWD_XCD): 0 = 2-D grid, else 1-D XCD ranges
 };
 
 struct eelg_sc_cfg {
@@ -55,6 +56,8 @@ struct eelg_sc_cfg {
   int nb;                        // nodes per fwd / grad-x workgroup
   int nth;                       // threads per fwd / grad-x workgroup
   int cld;                       // coefficient row stride (nterms rounded up to 16: 64-B aligned rows)
+  eelg_sc_bwdc_fn bwd_coefs;     // streaming coefficient gradient (round 6; nullptr: bwd_coef's chunk form)
+  int csets;                     // its term-group sets (workgroups per (channel, node range) tile)
 };
 
 // every generated tensor-product set, all channel counts (eelg_capi.hip merges the per-mul tables

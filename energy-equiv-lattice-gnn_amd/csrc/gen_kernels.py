@@ -73,6 +73,12 @@ TP_BWD_PFD = int(os.environ.get("EELG_TP_BWD_PFD", "2"))
 # tp_bwd (fp32): grad_w and gxe stored nontemporal (read back by later kernels: the sender sum,
 # the radial MLP backward on its side stream).  r04r: kbench 0.701 -> 0.683 ms, step +0.3-0.4 %
 TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "1"))
+# tp_bwd block placement: 0 = 2-D grid (edge block, input-block group), consecutive edge blocks
+# dealt round-robin over the 8 XCDs; 1 = 1-D grid, XCD k takes one contiguous range of edge
+# blocks with the groups of an edge block adjacent; 2 = the same ranges, group-major per XCD.
+# With 0 a receiver whose in-edges straddle two blocks has its grad_agg row fetched into two
+# L2s, and every XCD gathers every lattice's x rows
+TP_BWD_XCD = int(os.environ.get("EELG_TP_BWD_XCD", "2"))
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
@@ -115,6 +121,13 @@ SC_COEF_MAXJG = int(os.environ.get("EELG_SC_COEF_MAXJG", "64"))
 # coefficient gradient: term groups clustered by shared operands (coef_groups) instead of runs
 # of the term order
 SC_COEF_CLUSTER = int(os.environ.get("EELG_SC_COEF_CLUSTER", "1"))
+# coefficient gradient, streaming form (round 6): a wave owns ONE term group for a whole node
+# range, so its accumulators are zeroed and reduced across the lanes once per range instead of
+# once per 512-node chunk (the round-5 form spent ~21 % of its VALU instructions there); the
+# range's channel-major rows stream through two LDS buffers of SC_COEF_SC nodes filled by
+# LDS-DMA one chunk ahead.  0 = the round-5 chunk-resident kernel
+SC_COEF_STREAM = int(os.environ.get("EELG_SC_COEF_STREAM", "1"))
+SC_COEF_SC = 256                      # nodes per streamed chunk: one 1-KiB LDS-DMA row per wave-instruction
 # Variants built, measured slower and removed (DESIGN.md section 3 records the numbers): packed
 # channel-pair TP forward, 2x-unrolled TP edge loop, shared-coupling (M in LDS) and cooperative
 # TP forwards, two nodes / two channels per lane in the contraction, mul-major coefficient
@@ -623,23 +636,34 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     # cross-group reduction is needed; grad_w of every path is written once.
     bgroups = [[p for p in paths if p.l1 == l] for l in node_ls]
     bgroups = [g for g in bgroups if g]
+    NBG = len(bgroups) * CG
     L.append(f"__global__ __launch_bounds__(256) void tp_bwd_{name}{sfx}(")
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ receiver, int n_edges,")
     L.append("    const float* __restrict__ gagg, float inv_norm,")
     L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe, const int* __restrict__ spos) {{")
     L.append("  const int lane = threadIdx.x & 63;")
-    L += chan_head
+    if TP_BWD_XCD:
+        # 1-D grid of 8 * nb8 * NBG blocks (eelg_capi.hip); block b runs on XCD b % 8, which
+        # takes edge blocks [xcd * nb8, (xcd + 1) * nb8); surplus edge blocks exit below
+        L.append(f"  const int nb8 = gridDim.x / {8 * NBG}, xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;")
+        if TP_BWD_XCD == 1:
+            L.append(f"  const int by = bi % {NBG}, bx = xcd * nb8 + bi / {NBG};")
+        else:
+            L.append(f"  const int by = bi / nb8, bx = xcd * nb8 + bi % nb8;")
+    else:
+        L.append("  const int by = blockIdx.y, bx = blockIdx.x;")
+    L += [ln.replace("blockIdx.y", "by") for ln in chan_head]
     # spos (optional): gxe row of edge e is spos[e], its position in sender order, so the sender
     # sum reads gxe contiguously instead of gathering rows through sperm
     # a half-wave streams TP_BWD_EPH consecutive edges: while the last path of edge e
     # computes, edge e+1's x / SH rows and first path's grad_agg slice and weight are in
     # flight (its sender / receiver indices were loaded when edge e started)
     EPH = TP_BWD_EPH
-    L.append(f"  const int e0 = ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {EPH};")
+    L.append(f"  const int e0 = ((bx * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * {EPH};")
     L.append("  if (e0 >= n_edges) return;")
     L.append(f"  const int e1 = min(e0 + {EPH}, n_edges);")
-    L.append(f"  switch ({YSW}) {{")
+    L.append(f"  switch ({YSW.replace('blockIdx.y', 'by')}) {{")
     for gi, grp in enumerate(bgroups):
         l = grp[0].l1
         d = 2 * l + 1
@@ -835,7 +859,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  }")
     L.append("}")
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups) * CG, nbgroups=len(bgroups) * CG,
-                npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, fwpb=TP_FWD_WPB, sig=fnv1a64(tp_signature(node, sh, target)))
+                npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, fwpb=TP_FWD_WPB, bxcd=TP_BWD_XCD,
+                sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
 
@@ -902,6 +927,40 @@ def sc_blocks(plan, maxb: int = 32) -> List[Dict]:
     return blocks
 
 
+def _coef_cost(plan, g) -> int:
+    """issue cost of one term group per node: 4 x its operands (the LDS reads, round-2 model)
+    or its VALU count (one FMA per term + the shared pair / triple products), the larger"""
+    ops, prods = set(), set()
+    for t in g:
+        nu, (a, b, c), q = plan.terms[t]
+        ops |= {("x", a), ("g", q)} | ({("x", b)} if nu >= 2 else set()) | ({("x", c)} if nu >= 3 else set())
+        prods |= ({(a, b)} if nu >= 2 else set()) | ({(a, b, c)} if nu >= 3 else set())
+    return max(4 * len(ops), len(prods) + len(g))
+
+
+def coef_sets(plan, n_sets: int, n_waves: int, jg: int) -> List[List[int]]:
+    """Term groups of the streaming coefficient gradient: ``n_sets * n_waves`` clustered groups
+    (``coef_groups``), one per wave, returned in launch order (group s * n_waves + w = set s,
+    wave w).  Every chunk ends in a workgroup barrier, so a step lasts as long as the busiest
+    SIMD's waves; waves w, w + 4, w + 8, w + 12 share a SIMD (cyclic wave placement), so the
+    groups are dealt longest-first to the (set, w mod 4) bin with the least work."""
+    groups = [g for g in coef_groups(plan, 1, jg, n_sets * n_waves) if g]
+    assert len(groups) <= n_sets * n_waves, (len(groups), n_sets, n_waves)
+    per = n_waves // 4
+    bins = {(st, k): [] for st in range(n_sets) for k in range(4)}
+    load = {b: 0 for b in bins}
+    for g in sorted(groups, key=lambda g: _coef_cost(plan, g), reverse=True):
+        b = min((b for b in bins if len(bins[b]) < per), key=lambda b: load[b])
+        bins[b].append(g)
+        load[b] += _coef_cost(plan, g)
+    out = []
+    for st in range(n_sets):
+        for w in range(n_waves):
+            lst = bins[(st, w % 4)]
+            out.append(lst[w // 4] if w // 4 < len(lst) else [])
+    return out
+
+
 def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> List[List[int]]:
     """Term groups of the coefficient gradient, clustered so that a group reads few operands.
 
@@ -957,12 +1016,7 @@ def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> L
     assert len(groups) <= n_groups, (len(groups), n_groups)
 
     def cost(g):
-        ops, prods = set(), set()
-        for t in g:
-            nu, (a, b, c), q = terms[t]
-            ops |= {("x", a), ("g", q)} | ({("x", b)} if nu >= 2 else set()) | ({("x", c)} if nu >= 3 else set())
-            prods |= ({(a, b)} if nu >= 2 else set()) | ({(a, b, c)} if nu >= 3 else set())
-        return max(4 * len(ops), len(prods) + len(g))
+        return _coef_cost(plan, g)
     per = n_groups // n_waves
     load = [0] * n_waves
     slots: List[List[List[int]]] = [[] for _ in range(n_waves)]
@@ -1830,9 +1884,196 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("  }")
     L.append("}")
     WPB, NBC = WV, NCB
+    cstream = 0
+    if SC_COEF_STREAM:
+        L += emit_sc_coef_stream(name, plan, D, Dout, cld)
+        cstream, NBC = 1, SC_COEF_SC
     info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, cld=cld, njg=len(groups), wpb=WPB, nbc=NBC, nb=NB, nth=NTH,
-                cmajor_out=cmajor_out, sig=fnv1a64(sc_signature(coupling, ls, corr)))
+                cmajor_out=cmajor_out, cstream=cstream, csets=-(-nt // (16 * SC_COEF_MAXJG)),
+                sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
+
+
+def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[str]:
+    """Streaming coefficient gradient ``sc_bwd_coefs_<name>`` (round 6).
+
+    grad coef[c, t] = sum_n g_q(n) x_a(n) x_b(n) x_c(n) over the channel-major rows
+    xt[(c D + a) N + n] / gt[(c Dout + q) N + n].  A workgroup of 16 waves owns one tile
+    (channel c, node range r) and one of S term-group sets; wave w accumulates group s * 16 + w
+    (<= 64 terms, one lane per node of a 64-node sub-tile) over every node of the range, so its
+    accumulators are zeroed once and reduced across the 64 lanes once (eelg_lane_reduce64).  The
+    range's D + Dout rows stream through two LDS buffers of SC nodes: while chunk i is computed,
+    chunk i+1 arrives by LDS-DMA (one 1-KiB row per wave-instruction, no registers); a
+    ``vmcnt(0)`` and a barrier end each chunk.  The LDS operand reads are inline asm, so hipcc
+    does not drain the in-flight DMA before them.  A chunk that passes the range's end, or rows
+    that are not 16-B aligned (N % 4 != 0), are staged through registers with zero fill.
+    Three buffers: chunk i + 2 is issued while chunk i computes; each step opens with a counted
+    ``vmcnt`` (this wave's DMA for chunk i retired, chunk i + 1's still in flight) and a raw
+    ``s_barrier`` (a ``__syncthreads()`` would drain every DMA), and the buffer a step restages
+    was last read before that barrier (its reads retired by their own ``lgkmcnt(0)``).
+    Blocks: the S set-blocks of a tile are consecutive on one XCD (their rows cross HBM once,
+    then come from that XCD's L2).  part[r, c, t]: one deterministic partial per range."""
+    WV, SC = 16, SC_COEF_SC
+    nt = len(plan.terms)
+    S = -(-nt // (WV * SC_COEF_MAXJG))
+    JG = -(-nt // (WV * S))
+    assert JG <= 64
+    groups = coef_sets(plan, S, WV, JG)
+    ROWS = D + Dout
+    RB = SC * 4                                # bytes per LDS row (one wave-instruction)
+    assert RB == 1024 and (ROWS - 1) * (RB // 256) + SC // 64 - 1 <= 255
+    perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
+    L: List[str] = []
+    L.append(f"// streaming coefficient gradient: {S} sets x {WV} term groups of <= {JG} terms, "
+             f"{SC}-node chunks")
+    L.append(f"__device__ const short sc_coefs_perm_{name}[{len(perm)}] = {{")
+    for k in range(0, len(perm), 32):
+        L.append("  " + ", ".join(str(v) for v in perm[k: k + 32]) + ",")
+    L.append("};")
+    L.append(f"__global__ __launch_bounds__({64 * WV}) void sc_bwd_coefs_{name}(")
+    L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int rn,")
+    L.append("    float* __restrict__ part) {")
+    NBUF = 3
+    NW = -(-ROWS // WV)                        # most DMA rows a wave issues per chunk
+    L.append(f"  __shared__ __attribute__((aligned(16))) float sb_[{NBUF} * {ROWS} * {SC}];")
+    L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;")
+    L.append("  const int nr = (n_nodes + rn - 1) / rn;             // node ranges (partial rows)")
+    L.append(f"  const int q = blockIdx.x >> 3, st = q % {S};")
+    L.append("  const int tile = (q / " + str(S) + ") * 8 + (blockIdx.x & 7);")
+    L.append(f"  if (tile >= {MUL} * nr) return;                      // block-uniform")
+    L.append("  const int c = tile / nr, r = tile - c * nr;")
+    L.append("  const int nb0 = r * rn, nb1 = min(nb0 + rn, n_nodes);")
+    L.append(f"  const int jg = st * {WV} + wv;")
+    L.append("  const bool vec = (n_nodes & 3) == 0;")
+    L.append(f"  const float* __restrict__ xr = xt + (size_t)c * {D} * n_nodes;")
+    L.append(f"  const float* __restrict__ gr = gt + (size_t)c * {Dout} * n_nodes;")
+    L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float*)sb_);")
+    # staging of one chunk into buffer b
+    # stage(b, n0): chunk n0 into buffer b; returns the LDS-DMA instructions this wave issued
+    L.append("  auto stage = [&](int b, int n0) -> int {")
+    L.append("    if (n0 >= nb1) return 0;")
+    L.append(f"    float* __restrict__ dst = sb_ + b * {ROWS * SC};")
+    L.append(f"    if (vec && n0 + {SC} <= nb1) {{")
+    L.append("      int k = 0;")
+    L.append(f"      for (int row = wv; row < {ROWS}; row += {WV}, ++k) {{   // wave-uniform")
+    L.append(f"        const float* src = (row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes) + n0 + lane * 4;")
+    L.append("        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,")
+    L.append(f"            (__attribute__((address_space(3))) void*)(dst + row * {SC}), 16, 0, 0);")
+    L.append("      }")
+    L.append("      return k;")
+    L.append("    } else {")
+    L.append(f"      for (int i = threadIdx.x; i < {ROWS * SC}; i += {64 * WV}) {{")
+    L.append(f"        const int row = i / {SC}, j = i - row * {SC}, n = n0 + j;")
+    L.append(f"        const float* src = row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes;")
+    L.append("        dst[i] = n < nb1 ? src[n] : 0.0f;")
+    L.append("      }")
+    L.append('      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // stores done before the barrier')
+    L.append("      return 0;")
+    L.append("    }")
+    L.append("  };")
+    # counted wait: everything but this wave's ``p`` newest LDS-DMA instructions has landed
+    L.append("  auto retire = [&](int p) {")
+    for k in range(NW, 0, -1):
+        L.append(f'    {"if" if k == NW else "else if"} (p >= {k}) asm volatile("s_waitcnt vmcnt({k})" ::: "memory");')
+    L.append('    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+    L.append("  };")
+    L.append("  float acc[64];")
+    L.append("#pragma unroll")
+    L.append("  for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
+    L.append("  stage(0, nb0);")
+    L.append(f"  int pend = stage(1, nb0 + {SC});           // this wave's DMAs of the chunk after the current")
+    # the chunk loop sits inside each case: the accumulators never meet at a merge point inside
+    # the loop (a switch inside the loop made the compiler move all 64 of them at every case exit
+    # and spill); every wave, a group-less one too, runs the same stages and barriers
+    head = ["      int b = 0;",
+            f"      for (int n0 = nb0; n0 < nb1; n0 += {SC}, b = b == {NBUF - 1} ? 0 : b + 1) {{",
+            "        retire(pend);                         // chunk n0 landed (this wave's part)",
+            '        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");',
+            "        __builtin_amdgcn_s_barrier();        // every wave's part; the buffer restaged next is free",
+            f"        pend = stage(b == 0 ? 2 : b - 1, n0 + {2 * SC});",
+            f"        const unsigned ab = lds0 + b * {ROWS * RB} + lane * 4;"]
+    tail = ["      }",
+            '      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");']
+    L.append("  switch (jg) {")
+    for gi, grp in enumerate(groups):
+        if not grp:
+            continue
+        L.append(f"    case {gi}: {{")
+        L += head
+        need_x, need_g = set(), set()
+        for t in grp:
+            nu, (a, b_, cc), qq = plan.terms[t]
+            need_g.add(qq)
+            need_x.add(a)
+            if nu >= 2:
+                need_x.add(b_)
+            if nu >= 3:
+                need_x.add(cc)
+        ops = [("x", a, a) for a in sorted(need_x)] + [("g", qq, D + qq) for qq in sorted(need_g)]
+        cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
+        L.append("#pragma unroll 1")
+        L.append(f"      for (int sb = 0; sb < {SC // 64}; ++sb) {{")
+        L.append("        const unsigned a_ = ab + sb * 256;")
+        # operand reads: pairs of rows by ds_read2st64_b32 (offsets in 256-B units)
+        outs = []
+        for k in range(0, len(ops), 2):
+            pr = ops[k: k + 2]
+            if len(pr) == 2:
+                v = f"p{k // 2}"
+                L.append(f"        eelg_f2r {v};")
+                L.append(f'        asm volatile("ds_read2st64_b32 %0, %1 offset0:{pr[0][2] * (RB // 256)} '
+                         f'offset1:{pr[1][2] * (RB // 256)}" : "=v"({v}) : "v"(a_));')
+                outs.append(v)
+            else:
+                v = f"p{k // 2}s"
+                L.append(f"        float {v};")
+                L.append(f'        asm volatile("ds_read_b32 %0, %1 offset:{pr[0][2] * RB}" : "=v"({v}) : "v"(a_));')
+                outs.append(v)
+        for k in range(0, len(outs), 24):
+            L.append('        asm volatile("s_waitcnt lgkmcnt(0)" : ' +
+                     ", ".join(f'"+v"({v})' for v in outs[k: k + 24]) + ' : : "memory");')
+        for k in range(0, len(ops), 2):
+            pr = ops[k: k + 2]
+            if len(pr) == 2:
+                L.append(f"        const float {pr[0][0]}{pr[0][1]} = p{k // 2}[0], {pr[1][0]}{pr[1][1]} = p{k // 2}[1];")
+            else:
+                L.append(f"        const float {pr[0][0]}{pr[0][1]} = p{k // 2}s;")
+        order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
+        cur, curc = None, None
+        for jj in order:
+            t = grp[jj]
+            nu, (a, b_, cc), qq = plan.terms[t]
+            if nu == 1:
+                L.append(f"        acc[{jj}] = fmaf(x{a}, g{qq}, acc[{jj}]);")
+                continue
+            if cur != (a, b_):
+                if cur is not None:
+                    L.append("        }")
+                    L.append("        " + cpin)
+                L.append(f"        {{ const float pp = x{a} * x{b_};")
+                cur, curc = (a, b_), None
+            if nu == 2:
+                L.append(f"          acc[{jj}] = fmaf(pp, g{qq}, acc[{jj}]);")
+            else:
+                if curc != cc:
+                    L.append(f"          const float m{cc} = pp * x{cc};")
+                    curc = cc
+                L.append(f"          acc[{jj}] = fmaf(m{cc}, g{qq}, acc[{jj}]);")
+        if cur is not None:
+            L.append("        }")
+        L.append("        " + cpin)
+        L.append("      }")
+        L += tail
+        L.append("      break; }")
+    L.append("    default: {")
+    L += [ln for ln in head if "const unsigned ab" not in ln] + tail
+    L.append("      break; }")
+    L.append("  }")
+    L.append("  eelg_lane_reduce64(acc);")
+    L.append(f"  const int t = sc_coefs_perm_{name}[jg * 64 + lane];")
+    L.append(f"  if (t >= 0) part[((size_t)r * {MUL} + c) * {cld} + t] = acc[0];")
+    L.append("}")
+    return L
 
 
 # ---------------------------------------------------------------------------
@@ -1911,13 +2152,14 @@ def main(outdir: str) -> None:
                    else f"nullptr, nullptr, tp_bws_{name}, nullptr")
             parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                          f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                         f'{bfk}, {i["ngroups_bf"]}}},')
+                         f'{bfk}, {i["ngroups_bf"]}, {i["bxcd"]}}},')
         parts.append("};")
         parts.append("static const eelg_sc_cfg kScConfigs[] = {")
         for name, i in sc_table:
             parts.append(f'  {{"{name}", {i["D"]}, {i["Dout"]}, {i["drow"]}, {i["orow"]}, {i["nterms"]}, {i["njg"]}, {i["wpb"]}, '
                          f'0x{i["sig"]:016x}ULL, sc_fwd_{name}, sc_bwd_x_{name}, sc_bwd_coef_{name}, sc_cmajor_{name}, '
-                         f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}, {i["cld"]}}},')
+                         f'{i["cmajor_out"]}, {i["nbc"]}, {i["nb"]}, {i["nth"]}, {i["cld"]}, '
+                         f'{"sc_bwd_coefs_" + name if i["cstream"] else "nullptr"}, {i["csets"]}}},')
         parts.append("};")
         parts.append(f"const eelg_tp_cfg* eelg_tp_table_m{mul}(int* n) {{ *n = (int)(sizeof(kTpConfigs)/sizeof(kTpConfigs[0])); return kTpConfigs; }}")
         parts.append(f"const eelg_sc_cfg* eelg_sc_table_m{mul}(int* n) {{ *n = (int)(sizeof(kScConfigs)/sizeof(kScConfigs[0])); return kScConfigs; }}")

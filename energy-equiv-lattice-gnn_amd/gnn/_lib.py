@@ -54,6 +54,7 @@ _SIGS = {
     "eelg_sc_bwd_x": ([_I, _P, _P, _P, _I, _I, _P, _P], _I),
     "eelg_sc_bwd_x_cm": ([_I, _P, _P, _P, _I, _I, _P, _P, _P, _P], _I),
     "eelg_sc_bwd_coef": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
+    "eelg_sc_bwd_coef_parts": ([_I, _I, _I], _I),
     "eelg_sc_cmajor": ([_I, _I, _P, _I, _I, _P, _P], _I),
     "eelg_scg_fwd": ([_P, _P, _P, _I, _P, _I, _I, _P, _I, _P], _I),
     "eelg_scg_bwd_x": ([_P, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P], _I),

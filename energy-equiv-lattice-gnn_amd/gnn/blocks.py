@@ -28,6 +28,9 @@ from .o3 import Gate, GradMailbox, Linear, TensorProduct
 
 # the layer residual's gradient summed in linear_up's grad-x epilogue (1) or by autograd (0)
 RESIDUAL_GRAD_FUSED = os.environ.get("EELG_RESIDUAL_GRAD_FUSED", "1") != "0"
+# when a layer computes its own radial weights (in line, EELG_OVERLAP=0): run the radial MLP
+# before linear_up (1), so that tp_fwd directly follows the kernel that wrote its x, or after (0)
+RADIAL_FIRST = os.environ.get("EELG_RADIAL_FIRST", "1") != "0"
 
 EdgeIndex = Union[torch.Tensor, ops.EdgeCSR]
 
@@ -281,8 +284,12 @@ class TensorProductInteractionBlock(torch.nn.Module):
         stream, see ``GNN_Head``); computed here when not given."""
         csr, edge_attrs, edge_feats = as_csr(edge_index, node_feats.shape[0], edge_attrs, edge_feats)
         idx, info = self._config()
+        w = tp_weights
+        if w is None and RADIAL_FIRST:
+            w = self.radial_weights(edge_feats)
         x = self.linear_up(node_feats, grad_mailbox=grad_mailbox)
-        w = self.radial_weights(edge_feats) if tp_weights is None else tp_weights
+        if w is None:
+            w = self.radial_weights(edge_feats)
         inv = 1.0 / self.agg_norm_const
         if self.reduce in ("sum", "add"):
             agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv)

@@ -112,6 +112,7 @@ class _CGCConvEF(torch.autograd.Function):
         add done in the aggregation kernel's store and its gradient in grad-x's epilogue"""
         x = ops._f32(x).contiguous()
         ea = ops._f32(ea).contiguous()
+        ef = ops._f32(ef).contiguous()       # read as a raw [E, 8] fp32 array by the kernels
         n, d = x.shape
         if ef.shape != (csr.num_edges, 8) or ea.shape != (8, 2 * d) or n != csr.num_nodes:
             raise ValueError(f"CGC (factored edges) shapes: x {tuple(x.shape)}, ef {tuple(ef.shape)}, "

@@ -477,8 +477,8 @@ class _SymCon(torch.autograd.Function):
                 _lib.check(lib.eelg_sc_cmajor(ctx.cfg, 1, _lib.ptr(g), n, ctx.mul, _lib.ptr(gt),
                                               _lib.stream(gt)), "sc_cmajor")
                 TIMER.stop(tok)
-            chunk = ctx.info["coef_chunk"]          # LDS-resident nodes per workgroup
-            nch = (n + chunk - 1) // chunk
+            chunk = ctx.info["coef_chunk"]          # nodes per streamed (LDS-staged) chunk
+            nch = int(lib.eelg_sc_bwd_coef_parts(ctx.cfg, n, ctx.mul))   # partial rows (node ranges)
             part = torch.empty(nch, ctx.mul, ctx.info["coef_ld"], device=x.device, dtype=torch.float32)
             if ctx.info["coef_ld"] != ctx.info["nterms"]:
                 part[:, :, ctx.info["nterms"]:].zero_()   # the kernel writes terms < nterms

@@ -236,13 +236,16 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
                    void* stream);
 /* Coefficient gradient (replaces the weight gradient through the U.W contraction of
  * gnn/mace.py:242-277) from the channel-major copies xt[(c*D + a)*N + n] / gt of x and
- * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_chunks, mul, coef_ld] (the
- * entries past nterms of each row are not written),
- * n_chunks = ceil(n_nodes / chunk); chunk must be the config's coef_chunk (info[6]): one
- * workgroup keeps that many nodes of one channel resident in LDS.  The caller sums over
- * chunks (deterministic). */
+ * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_parts, mul, coef_ld] (the
+ * entries past nterms of each row are not written), n_parts = eelg_sc_bwd_coef_parts(cfg,
+ * n_nodes, mul): one partial per node range (streaming kernel: at most 4 ranges of whole
+ * coef_chunk-node chunks; round-5 chunk kernel: one per coef_chunk nodes).  chunk must be the
+ * config's coef_chunk (info[6]).  The caller sums over the partials (deterministic).
+ * Non-overlapping xt / gt; 16-byte aligned rows (n_nodes % 4 == 0) take the LDS-DMA path. */
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes,
                      int mul, int chunk, float* partial, void* stream);
+/* The number of partial rows eelg_sc_bwd_coef writes for n_nodes (-1: unknown config). */
+int eelg_sc_bwd_coef_parts(int cfg, int n_nodes, int mul);
 
 /* Symmetric contraction from a term table (correlation 4: U_matrix_real with filter_ir_mid,
  * gnn/mace.py:435-477; the contraction itself gnn/mace.py:242-277).  Replaces

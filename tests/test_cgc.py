@@ -64,8 +64,11 @@ def _rel(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("reduction,d", [("sum", 128), ("mean", 64), ("sum", 96)])
+@pytest.mark.parametrize("reduction,d", [("sum", 128), ("mean", 64), ("sum", 96), ("sum", 192),
+                                         ("mean", 256)])
 def test_cgc_layer_fwd_bwd(reduction, d):
+    """One CGC layer against the fp64 oracle, every node width class of the kernels: D <= 64
+    (1 float per lane), <= 128 (2) and <= 256 (4 floats per lane, CGC_MAXD)."""
     from gnn.cgc import CGCLayer
     torch.manual_seed(1)
     o = ocgc.CGCLayer(d, d, reduction).double()
@@ -174,7 +177,8 @@ def test_dense_linear_matches_torch(k, n_out, bias, rows):
 
 
 @pytest.mark.gpu
-def test_cgc_factored_edges_match_generic_layer():
+@pytest.mark.parametrize("d", [128, 192, 256])
+def test_cgc_factored_edges_match_generic_layer(d):
     """``CGCLayer.forward_factored`` (edge features as [e5 | 1] @ A, eelg_cgc_fwd_ef) equals the
     generic ``forward`` on the materialised edge features e5 W5^T + b5 (two fp32 evaluations in
     different association orders: 1e-5 of the largest entry), gradients w.r.t. x and the layer
@@ -182,7 +186,6 @@ def test_cgc_factored_edges_match_generic_layer():
     from gnn import cgc
     from gnn.model import EnergyEquivGNN
     torch.manual_seed(4)
-    d = 128
     layer = cgc.CGCLayer(d, d).cuda()
     emb = torch.nn.Linear(5, d).cuda()
     b, _ = batch(3, 40, 160, 17)
@@ -209,7 +212,7 @@ def test_cgc_factored_edges_match_generic_layer():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,reduction", [(128, "sum"), (64, "mean")])
+@pytest.mark.parametrize("d,reduction", [(128, "sum"), (64, "mean"), (192, "sum"), (256, "mean")])
 def test_cgc_fused_residual_matches_explicit_add(d, reduction):
     """``forward_factored(..., residual=True)`` (x + layer(x) with the add in the aggregation
     kernel's store and its gradient in grad-x's epilogue) equals the explicit ``x + layer(x)``:
@@ -266,3 +269,34 @@ def test_small_in_linear_matches_fp64(k, n_out, bias, rows):
     assert rel(lin.weight.grad, w64.grad) < 2e-6
     if bias:
         assert rel(lin.bias.grad, b64.grad) < 2e-6
+
+
+@pytest.mark.gpu
+def test_cgc_softplus_sigmoid_match_torch_over_the_range():
+    """The kernels' fast-math softplus and sigmoid (hardware exp2 / log2 / rcp, CGC_FAST_MATH)
+    against torch's fp64 softplus (threshold 20) and sigmoid over z in [-30, 20], through the
+    C-ABI forward: one self-edge per receiver, ps = ep = 0, pr = [zv | zm], so
+    agg = softplus(zv) * sigmoid(zm).  With zm = 40 (sigmoid = 1.0f) agg is softplus alone,
+    relative error <= 5e-6 everywhere, including z < -16.6 where softplus ~ exp(z) (the bound is
+    the fp32 rounding of the exp2 argument, |z| log2(e) 2^-24 ln 2 = 1.8e-6 at z = -30); with
+    zv = 30 (softplus = z) agg is 30 * sigmoid(zm)."""
+    from gnn import _lib
+    lib = _lib.load()
+    d = 64
+    z = torch.linspace(-30.0, 20.0, 4096 * d, dtype=F64).reshape(-1, d)
+    n = z.shape[0]
+    rowptr = torch.arange(n + 1, dtype=torch.int32, device="cuda")
+    sender = torch.arange(n, dtype=torch.int32, device="cuda")
+    ps = torch.zeros(n, 2 * d, device="cuda")
+    ep = torch.zeros(n, 2 * d, device="cuda")
+    for which in ("softplus", "sigmoid"):
+        zf = z.float()
+        fixed = torch.full_like(zf, 40.0 if which == "softplus" else 30.0)
+        pr = (torch.cat([zf, fixed], 1) if which == "softplus" else torch.cat([fixed, zf], 1)).cuda().contiguous()
+        agg = torch.empty(n, d, device="cuda")
+        _lib.check(lib.eelg_cgc_fwd(_lib.ptr(ps), _lib.ptr(pr), _lib.ptr(ep), _lib.ptr(sender),
+                                    _lib.ptr(rowptr), None, n, d, _lib.ptr(agg), _lib.stream(agg)), "cgc_fwd")
+        zr = zf.double()
+        ref = (torch.nn.functional.softplus(zr) if which == "softplus" else 30.0 * torch.sigmoid(zr))
+        rel = ((agg.double().cpu() - ref).abs() / ref.abs()).max().item()
+        assert rel < 5e-6, (which, rel)

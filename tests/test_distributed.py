@@ -1,4 +1,5 @@
-"""Graph-sharded data parallelism on CPU with gloo, world_size 2.
+"""Graph-sharded data parallelism on CPU with gloo, world sizes 2 and 8 (SURVEY.md 4.5, 8e;
+8 = BASELINE config 3's rank count, ``scripts/train_main.py:89-100``).
 
 Checks that sharding whole graphs across ranks + one flat gradient all-reduce
 (``gnn.parallel.FlatGradAllReduce``) reproduces the single-process full-batch
@@ -9,6 +10,7 @@ import os
 import socket
 import tempfile
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -25,9 +27,9 @@ def _free_port():
     return p
 
 
-def _graphs():
+def _graphs(n=4):
     from gnn.synthetic import SyntheticLattices
-    return SyntheticLattices(4, 24, 96, 77)
+    return SyntheticLattices(n, 24, 96, 77)
 
 
 def _model(seed):
@@ -36,7 +38,7 @@ def _model(seed):
     return omodel.EnergyEquivGNN(small_params(max_edge_radius=_graphs().max_edge_radius)).double()
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, per_rank=2):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,8 +48,8 @@ def _worker(rank, world, port, out):
     from oracle.train import stiffness_loss
     m = _model(seed=rank + 100)          # deliberately different init per rank
     broadcast_parameters(m)              # -> rank 0's weights everywhere
-    ds = _graphs()
-    idx = shard_indices(len(ds), rank, world, per_rank=2)
+    ds = _graphs(world * per_rank)
+    idx = shard_indices(len(ds), rank, world, per_rank=per_rank)
     b = batch_to(collate([ds[i] for i in idx]), "cpu", torch.float64)
     loss = stiffness_loss(m(b)["stiffness"], b.stiffness)
     loss.backward()
@@ -59,11 +61,14 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_sharded_allreduce_matches_full_batch_gradient():
-    world = 2
+@pytest.mark.parametrize("world,per_rank", [(2, 2), (8, 1)])
+def test_sharded_allreduce_matches_full_batch_gradient(world, per_rank):
+    """``world`` gloo ranks, each with ``per_rank`` whole graphs and its own init (replaced by
+    rank 0's through ``broadcast_parameters``): after one flat all-reduce rank 0's averaged
+    gradient equals the single-process gradient of the whole ``world * per_rank``-graph batch."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "grads.pt")
-        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), out, per_rank), nprocs=world, join=True)
         grads = torch.load(out, weights_only=True)
         weights = torch.load(out + ".w", weights_only=True)
     from gnn.data import collate
@@ -71,8 +76,8 @@ def test_sharded_allreduce_matches_full_batch_gradient():
     m = _model(seed=100)                 # rank 0's init
     for k, p in m.named_parameters():
         assert torch.equal(p.detach(), weights[k]), k
-    ds = _graphs()
-    b = batch_to(collate([ds[i] for i in range(4)]), "cpu", torch.float64)
+    ds = _graphs(world * per_rank)
+    b = batch_to(collate([ds[i] for i in range(world * per_rank)]), "cpu", torch.float64)
     loss = stiffness_loss(m(b)["stiffness"], b.stiffness)
     loss.backward()
     for k, p in m.named_parameters():

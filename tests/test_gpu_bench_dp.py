@@ -21,10 +21,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(*extra, timeout=300):
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+def _run(*extra, timeout=300, gpus=2, steps=3, env=None):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", str(steps),
            "--warmup", "1", "--no-cpu-baseline", *extra]
-    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                          env=None if env is None else {**os.environ, **env})
 
 
 def test_bench_two_ranks_reports_dp2_and_keeps_replicas_identical():
@@ -51,3 +52,29 @@ def test_bench_refuses_a_multi_rank_headline_over_gloo():
     r = _run(timeout=200)
     assert r.returncode != 0
     assert "refusing" in (r.stderr + r.stdout)
+
+
+def test_bench_eight_ranks_config3_shape():
+    """BASELINE config 3's shape through the bench's own launcher: 8 ranks x 32 graphs x 1024
+    nodes = global batch 256, 2 timed AdamW steps.  On a box with fewer than 8 GPUs the ranks
+    share the device over gloo (``--rehearsal``, about 8 GB of HBM per rank): that exercises the
+    8-rank sharding, broadcast, flat all-reduce and replica consistency on the HIP path; the
+    RCCL measurement is the 8-GPU driver run's."""
+    ndev = torch.cuda.device_count()
+    extra = ["--check-params"] + ([] if ndev >= 8 else ["--rehearsal"])
+    # 8 processes on one device: two hardware queues each (16 in all) instead of the default 4,
+    # so the device's queue slots are not oversubscribed (r08b: at 8 x 4 queues one rank's
+    # kernels failed to launch)
+    r = _run(*extra, gpus=8, steps=2, timeout=600,
+             env=None if ndev >= 8 else {"GPU_MAX_HW_QUEUES": "2"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["ranks"] == 8
+    assert out["config"]["parallelism"] == "graph-sharded dp8"
+    assert out["config"]["global_batch"] == 256
+    assert out["rehearsal"] == (ndev < 8)
+    assert out["backend"] == ("nccl" if ndev >= 8 else "gloo")
+    assert out["params_equal_across_ranks"] is True
+    assert math.isfinite(out["value"]) and out["value"] > 0 and math.isfinite(out["loss"])

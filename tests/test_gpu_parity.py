@@ -422,12 +422,15 @@ def test_stream_overlap_matches_in_line_bitwise():
         assert torch.equal(g0, g1)
 
 
-@pytest.mark.parametrize("lmax,n", [(4, 1), (4, 300), (4, 513), (4, 2051), (3, 1027)])
+@pytest.mark.parametrize("lmax,n", [(4, 1), (4, 300), (4, 513), (4, 2051), (3, 1027), (4, 2052),
+                                    (4, 9000), (4, 12288), (3, 8196)])
 def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
-    """eelg_sc_bwd_coef over several LDS-resident node chunks (a ragged last chunk, n not a
-    multiple of 4) against the fp64 sum over nodes of g_q x_a x_b x_c per polynomial term
-    (SURVEY 8c per-kernel tolerance 1e-5, reduction order only).  The partial buffer starts
-    as NaN, so a chunk or term the kernel skips fails the test."""
+    """eelg_sc_bwd_coef over several node ranges and streamed chunks against the fp64 sum over
+    nodes of g_q x_a x_b x_c per polynomial term (SURVEY 8c per-kernel tolerance 1e-5, reduction
+    order only): LDS-DMA chunks (n % 4 == 0), a ragged last chunk staged through registers
+    (300, 2052, 9000, 8196), rows that are not 16-B aligned (n % 4 != 0: every chunk through
+    registers), one to three node ranges.  The partial buffer starts as NaN, so a range or term
+    the kernel skips fails the test."""
     from gnn import _lib, cg
     from gnn.mace import SymmetricContraction
     hid = "+".join(f"32x{l}{'e' if l % 2 == 0 else 'o'}" for l in range(lmax + 1))
@@ -447,9 +450,10 @@ def test_symcon_coef_grad_kernel_vs_fp64(lmax, n):
         return torch.cat(blocks, 2).permute(1, 2, 0).contiguous()          # [32, D, n]
     xt, gt = cmajor(x), cmajor(g)
     ops_x, ops_g = xt, gt
-    nch = -(-n // chunk)
-    part = torch.full((nch, 32, info["coef_ld"]), float("nan"), device=DEV)
     lib = _lib.load()
+    nch = int(lib.eelg_sc_bwd_coef_parts(idx, n, 32))
+    assert 1 <= nch <= max(1, -(-n // chunk))
+    part = torch.full((nch, 32, info["coef_ld"]), float("nan"), device=DEV)
     _lib.check(lib.eelg_sc_bwd_coef(idx, _lib.ptr(ops_x), _lib.ptr(ops_g), n, 32, chunk, _lib.ptr(part),
                                     _lib.stream(part)), "sc_bwd_coef")
     got = part.sum(0)[:, :nt]

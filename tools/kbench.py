@@ -159,7 +159,7 @@ def main():
     cm()
     ops._lib.check(lib.eelg_sc_cmajor(sidx, 1, ops._lib.ptr(gs), n, 32, ops._lib.ptr(gt), ops._lib.stream(x)), "cm")
     chunk = sinfo["coef_chunk"]                                     # as gnn/ops.py
-    nch = (n + chunk - 1) // chunk
+    nch = int(lib.eelg_sc_bwd_coef_parts(sidx, n, 32))
     part = torch.empty(nch, 32, sinfo["coef_ld"], device=dev)
 
     def scbc():
