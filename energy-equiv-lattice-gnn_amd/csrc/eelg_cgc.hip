@@ -48,9 +48,13 @@ __device__ __forceinline__ float cgc_sigmoid(float z) { return 1.0f / (1.0f + ex
 // a multiple of 8, logical block (b % 8) * (gridDim.x / 8) + b / 8 hands XCD k one contiguous
 // range of receivers, i.e. whole lattices in order, so a lattice's gathered Ps rows (1 KiB per
 // node at D = 128, 1 MiB per 1024-node lattice) are fetched into one L2 and re-read there by
-// the node's other out-edges, instead of being fetched by all eight L2s
+// the node's other out-edges, instead of being fetched by all eight L2s.
+// Measured (r08d, cgc_modified, batch 256): cgc_fwd reads 1,328 -> 704 MB per launch and the
+// streaming backward 1,433 -> 916 MB, but every CGC kernel ran ~1 % slower and the step 1.8 %
+// slower (32,446 vs 33,033 graphs/s over three alternating pairs): the re-fetches it removes
+// were served by the Infinity Cache, so the default keeps the round-robin order (0)
 #ifndef CGC_XCD
-#define CGC_XCD 1
+#define CGC_XCD 0
 #endif
 __device__ __forceinline__ int cgc_block() {
 #if CGC_XCD

@@ -2014,50 +2014,69 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
         L.append("#pragma unroll 1")
         L.append(f"      for (int sb = 0; sb < {SC // 64}; ++sb) {{")
         L.append("        const unsigned a_ = ab + sb * 256;")
-        # operand reads: pairs of rows by ds_read2st64_b32 (offsets in 256-B units)
-        outs = []
-        for k in range(0, len(ops), 2):
-            pr = ops[k: k + 2]
-            if len(pr) == 2:
-                v = f"p{k // 2}"
-                L.append(f"        eelg_f2r {v};")
-                L.append(f'        asm volatile("ds_read2st64_b32 %0, %1 offset0:{pr[0][2] * (RB // 256)} '
-                         f'offset1:{pr[1][2] * (RB // 256)}" : "=v"({v}) : "v"(a_));')
-                outs.append(v)
-            else:
-                v = f"p{k // 2}s"
-                L.append(f"        float {v};")
-                L.append(f'        asm volatile("ds_read_b32 %0, %1 offset:{pr[0][2] * RB}" : "=v"({v}) : "v"(a_));')
-                outs.append(v)
-        for k in range(0, len(outs), 24):
-            L.append('        asm volatile("s_waitcnt lgkmcnt(0)" : ' +
-                     ", ".join(f'"+v"({v})' for v in outs[k: k + 24]) + ' : : "memory");')
-        for k in range(0, len(ops), 2):
-            pr = ops[k: k + 2]
-            if len(pr) == 2:
-                L.append(f"        const float {pr[0][0]}{pr[0][1]} = p{k // 2}[0], {pr[1][0]}{pr[1][1]} = p{k // 2}[1];")
-            else:
-                L.append(f"        const float {pr[0][0]}{pr[0][1]} = p{k // 2}s;")
+        # operand reads: pairs of rows by ds_read2st64_b32 (offsets in 256-B units), in the
+        # order the terms first use them; each operand is waited for (counted lgkmcnt) just
+        # before its first use, so the FMAs start while the later reads are in flight
         order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
+        seq = []
+        for jj in order:
+            nu, (a, b_, cc), qq = plan.terms[grp[jj]]
+            for o in ([("x", a), ("g", qq)] if nu == 1 else
+                      [("x", a), ("x", b_)] + ([("x", cc)] if nu == 3 else []) + [("g", qq)]):
+                if o not in seq:
+                    seq.append(o)
+        row = {("x", a): a for a in need_x} | {("g", qq): D + qq for qq in need_g}
+        reads = [seq[k: k + 2] for k in range(0, len(seq), 2)]
+        ridx = {o: k for k, rd in enumerate(reads) for o in rd}
+        L.append("        float " + ", ".join(f"{o[0]}{o[1]}" for o in seq) + ";")
+        for k, rd in enumerate(reads):
+            if len(rd) == 2:
+                L.append(f"        eelg_f2r p{k};")
+                L.append(f'        asm volatile("ds_read2st64_b32 %0, %1 offset0:{row[rd[0]] * (RB // 256)} '
+                         f'offset1:{row[rd[1]] * (RB // 256)}" : "=v"(p{k}) : "v"(a_));')
+            else:
+                L.append(f"        float p{k};")
+                L.append(f'        asm volatile("ds_read_b32 %0, %1 offset:{row[rd[0]] * RB}" : "=v"(p{k}) : "v"(a_));')
+        state = {"w": -1}
+
+        def need(*opsn):
+            k = max(ridx[o] for o in opsn)
+            if k <= state["w"]:
+                return
+            regs = [f"p{j}" for j in range(state["w"] + 1, k + 1)]
+            L.append(f'        asm volatile("s_waitcnt lgkmcnt({len(reads) - 1 - k})" : ' +
+                     ", ".join(f'"+v"({v})' for v in regs) + ' : : "memory");')
+            for j in range(state["w"] + 1, k + 1):
+                rd = reads[j]
+                if len(rd) == 2:
+                    L.append(f"        {rd[0][0]}{rd[0][1]} = p{j}[0]; {rd[1][0]}{rd[1][1]} = p{j}[1];")
+                else:
+                    L.append(f"        {rd[0][0]}{rd[0][1]} = p{j};")
+            state["w"] = k
         cur, curc = None, None
         for jj in order:
             t = grp[jj]
             nu, (a, b_, cc), qq = plan.terms[t]
             if nu == 1:
+                need(("x", a), ("g", qq))
                 L.append(f"        acc[{jj}] = fmaf(x{a}, g{qq}, acc[{jj}]);")
                 continue
             if cur != (a, b_):
                 if cur is not None:
                     L.append("        }")
                     L.append("        " + cpin)
+                need(("x", a), ("x", b_))
                 L.append(f"        {{ const float pp = x{a} * x{b_};")
                 cur, curc = (a, b_), None
             if nu == 2:
+                need(("g", qq))
                 L.append(f"          acc[{jj}] = fmaf(pp, g{qq}, acc[{jj}]);")
             else:
                 if curc != cc:
+                    need(("x", cc))
                     L.append(f"          const float m{cc} = pp * x{cc};")
                     curc = cc
+                need(("g", qq))
                 L.append(f"          acc[{jj}] = fmaf(m{cc}, g{qq}, acc[{jj}]);")
         if cur is not None:
             L.append("        }")
