@@ -128,6 +128,12 @@ SC_COEF_CLUSTER = int(os.environ.get("EELG_SC_COEF_CLUSTER", "1"))
 # LDS-DMA one chunk ahead.  0 = the round-5 chunk-resident kernel
 SC_COEF_STREAM = int(os.environ.get("EELG_SC_COEF_STREAM", "1"))
 SC_COEF_SC = 256                      # nodes per streamed chunk: one 1-KiB LDS-DMA row per wave-instruction
+# streamed image as row pairs read by ds_read_b64 (1), or as rows read by ds_read2st64_b32 (0).
+# Measured (kbench, same boxes): rows 0.402-0.404 ms; pairs 0.578 ms (r08f, the DMA issue loop
+# with per-instruction divisions) and 0.464 ms (r08g, strength-reduced issue: 208 four-byte
+# LDS-DMA instructions per chunk instead of 50 sixteen-byte ones, SALU 55 -> 88 M, issue
+# stalls 186 -> 260 M per launch) -- the halved LDS read cycles do not pay for the fill
+SC_COEF_PAIRS = int(os.environ.get("EELG_SC_COEF_PAIRS", "0"))
 # Variants built, measured slower and removed (DESIGN.md section 3 records the numbers): packed
 # channel-pair TP forward, 2x-unrolled TP edge loop, shared-coupling (M in LDS) and cooperative
 # TP forwards, two nodes / two channels per lane in the contraction, mul-major coefficient
@@ -944,7 +950,7 @@ def coef_sets(plan, n_sets: int, n_waves: int, jg: int) -> List[List[int]]:
     wave w).  Every chunk ends in a workgroup barrier, so a step lasts as long as the busiest
     SIMD's waves; waves w, w + 4, w + 8, w + 12 share a SIMD (cyclic wave placement), so the
     groups are dealt longest-first to the (set, w mod 4) bin with the least work."""
-    groups = [g for g in coef_groups(plan, 1, jg, n_sets * n_waves) if g]
+    groups = [g for g in coef_groups(plan, 1, jg, n_sets * n_waves, pairs=bool(SC_COEF_PAIRS)) if g]
     assert len(groups) <= n_sets * n_waves, (len(groups), n_sets, n_waves)
     per = n_waves // 4
     bins = {(st, k): [] for st in range(n_sets) for k in range(4)}
@@ -961,7 +967,8 @@ def coef_sets(plan, n_sets: int, n_waves: int, jg: int) -> List[List[int]]:
     return out
 
 
-def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> List[List[int]]:
+def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2,
+                pairs: bool = False) -> List[List[int]]:
     """Term groups of the coefficient gradient, clustered so that a group reads few operands.
 
     A lane (one node) of a group loads every x_a / g_q the group's terms use from LDS once per
@@ -981,13 +988,16 @@ def coef_groups(plan, n_waves: int, jg: int, n_groups: int, lds_w: int = 2) -> L
     abcid = np.full(nt, -1, dtype=np.int64)
     ab_ix, abc_ix = {}, {}
     nx = 1 + max(max(a, b, c) for _, (a, b, c), _ in terms)
+    # pairs: an operand costs its LDS row pair (rows 2p, 2p + 1: one ds_read_b64 of the
+    # streaming kernel's image), so the groups gather operands whose partner row is used too
+    f = (lambda i: i // 2) if pairs else (lambda i: i)  # noqa: E731
     for t, (nu, (a, b, c), q) in enumerate(terms):
-        m = (1 << a) | (1 << (nx + q))
+        m = (1 << f(a)) | (1 << (nx + f(q)))
         if nu >= 2:
-            m |= 1 << b
+            m |= 1 << f(b)
             abid[t] = ab_ix.setdefault((a, b), len(ab_ix))
         if nu >= 3:
-            m |= 1 << c
+            m |= 1 << f(c)
             abcid[t] = abc_ix.setdefault((a, b, c), len(abc_ix))
         opm[t] = m
     assert 2 * nx <= 64
@@ -1901,31 +1911,51 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     xt[(c D + a) N + n] / gt[(c Dout + q) N + n].  A workgroup of 16 waves owns one tile
     (channel c, node range r) and one of S term-group sets; wave w accumulates group s * 16 + w
     (<= 64 terms, one lane per node of a 64-node sub-tile) over every node of the range, so its
-    accumulators are zeroed once and reduced across the 64 lanes once (eelg_lane_reduce64).  The
-    range's D + Dout rows stream through two LDS buffers of SC nodes: while chunk i is computed,
-    chunk i+1 arrives by LDS-DMA (one 1-KiB row per wave-instruction, no registers); a
-    ``vmcnt(0)`` and a barrier end each chunk.  The LDS operand reads are inline asm, so hipcc
-    does not drain the in-flight DMA before them.  A chunk that passes the range's end, or rows
-    that are not 16-B aligned (N % 4 != 0), are staged through registers with zero fill.
-    Three buffers: chunk i + 2 is issued while chunk i computes; each step opens with a counted
-    ``vmcnt`` (this wave's DMA for chunk i retired, chunk i + 1's still in flight) and a raw
-    ``s_barrier`` (a ``__syncthreads()`` would drain every DMA), and the buffer a step restages
-    was last read before that barrier (its reads retired by their own ``lgkmcnt(0)``).
-    Blocks: the S set-blocks of a tile are consecutive on one XCD (their rows cross HBM once,
-    then come from that XCD's L2).  part[r, c, t]: one deterministic partial per range."""
+    accumulators are zeroed once and reduced across the 64 lanes once (eelg_lane_reduce64).
+
+    The range streams through three LDS buffers of SC nodes filled by LDS-DMA two chunks ahead
+    (no registers): each step opens with a counted ``vmcnt`` (this wave's DMA of the current
+    chunk retired, the next chunk's still in flight) and a raw ``s_barrier`` (a
+    ``__syncthreads()`` would drain every DMA); the buffer the step restages was last read before
+    that barrier, its reads retired by their own ``lgkmcnt``.  Operand reads are inline asm (so
+    hipcc does not drain the in-flight DMA before them), issued in the order the terms first use
+    them, each waited for by a counted ``lgkmcnt`` just before its first use.
+    SC_COEF_PAIRS (round 6): the image is [row pair][node][2] -- rows 2p and 2p + 1 of a node side
+    by side -- so one ``ds_read_b64`` (2 LDS cycles) returns two operands, where the row image
+    needed a ``ds_read2st64_b32`` (4 cycles); the pairs are filled by 4-byte LDS-DMA, 32 nodes x
+    2 rows per wave-instruction (per-lane source offset fixed per workgroup).  An odd row count
+    pads its last pair with a copy of its first row (never read).
+    A chunk that passes the range's end, or rows that are not 16-B aligned (N % 4 != 0), are
+    staged through registers with zero fill.  Blocks: the S set-blocks of a tile are consecutive
+    on one XCD (their rows cross HBM once, then come from that XCD's L2).  part[r, c, t]: one
+    deterministic partial per range."""
     WV, SC = 16, SC_COEF_SC
+    PAIRS = SC_COEF_PAIRS
     nt = len(plan.terms)
     S = -(-nt // (WV * SC_COEF_MAXJG))
     JG = -(-nt // (WV * S))
     assert JG <= 64
     groups = coef_sets(plan, S, WV, JG)
     ROWS = D + Dout
-    RB = SC * 4                                # bytes per LDS row (one wave-instruction)
-    assert RB == 1024 and (ROWS - 1) * (RB // 256) + SC // 64 - 1 <= 255
+    NBUF = 3
+    PX, PG = -(-D // 2), -(-Dout // 2)        # row pairs of x and of g (PAIRS)
+    if PAIRS:
+        NP = PX + PG
+        BUFF = NP * SC * 2                     # floats per buffer
+        NINS = NP * (SC // 32)                 # 4-byte DMA instructions per chunk (32 nodes x 2 rows)
+        PB = SC * 8                            # bytes per pair block
+        assert (NP - 1) * PB + (SC // 64 - 1) * 512 <= 65535
+        NW = -(-NINS // WV)
+    else:
+        BUFF = ROWS * SC
+        RB = SC * 4                            # bytes per LDS row (one wave-instruction)
+        assert RB == 1024 and (ROWS - 1) * (RB // 256) + SC // 64 - 1 <= 255
+        NW = -(-ROWS // WV)                    # most DMA rows a wave issues per chunk
+    assert NBUF * BUFF * 4 <= 163840
     perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
     L: List[str] = []
     L.append(f"// streaming coefficient gradient: {S} sets x {WV} term groups of <= {JG} terms, "
-             f"{SC}-node chunks")
+             f"{SC}-node chunks, {'row-pair' if PAIRS else 'row'} image")
     L.append(f"__device__ const short sc_coefs_perm_{name}[{len(perm)}] = {{")
     for k in range(0, len(perm), 32):
         L.append("  " + ", ".join(str(v) for v in perm[k: k + 32]) + ",")
@@ -1933,9 +1963,7 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     L.append(f"__global__ __launch_bounds__({64 * WV}) void sc_bwd_coefs_{name}(")
     L.append("    const float* __restrict__ xt, const float* __restrict__ gt, int n_nodes, int rn,")
     L.append("    float* __restrict__ part) {")
-    NBUF = 3
-    NW = -(-ROWS // WV)                        # most DMA rows a wave issues per chunk
-    L.append(f"  __shared__ __attribute__((aligned(16))) float sb_[{NBUF} * {ROWS} * {SC}];")
+    L.append(f"  __shared__ __attribute__((aligned(16))) float sb_[{NBUF * BUFF}];")
     L.append("  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;")
     L.append("  const int nr = (n_nodes + rn - 1) / rn;             // node ranges (partial rows)")
     L.append(f"  const int q = blockIdx.x >> 3, st = q % {S};")
@@ -1948,24 +1976,52 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     L.append(f"  const float* __restrict__ xr = xt + (size_t)c * {D} * n_nodes;")
     L.append(f"  const float* __restrict__ gr = gt + (size_t)c * {Dout} * n_nodes;")
     L.append("  const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) float*)sb_);")
-    # staging of one chunk into buffer b
+    if PAIRS:
+        # DMA instruction i = wv + 16 k of a chunk moves pair i / NB32, node block i % NB32; with
+        # NB32 = 8 a wave keeps node block nb = wv & 7 and walks pairs h, h + 2, ... (h = wv >> 3).
+        # Lane l: node 32 nb + l / 2 of row 2p + l % 2 (its element offset lo2, fixed per wave);
+        # the pad row of an odd array repeats row 2p (lo1: in bounds, never read)
+        assert SC // 32 == 8 and WV == 16
+        L.append("  const int h = wv >> 3, nbk = wv & 7;")
+        L.append("  const int lo2 = (lane & 1) * n_nodes + nbk * 32 + (lane >> 1), lo1 = nbk * 32 + (lane >> 1);")
     # stage(b, n0): chunk n0 into buffer b; returns the LDS-DMA instructions this wave issued
     L.append("  auto stage = [&](int b, int n0) -> int {")
     L.append("    if (n0 >= nb1) return 0;")
-    L.append(f"    float* __restrict__ dst = sb_ + b * {ROWS * SC};")
+    L.append(f"    float* __restrict__ dst = sb_ + b * {BUFF};")
     L.append(f"    if (vec && n0 + {SC} <= nb1) {{")
     L.append("      int k = 0;")
-    L.append(f"      for (int row = wv; row < {ROWS}; row += {WV}, ++k) {{   // wave-uniform")
-    L.append(f"        const float* src = (row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes) + n0 + lane * 4;")
-    L.append("        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,")
-    L.append(f"            (__attribute__((address_space(3))) void*)(dst + row * {SC}), 16, 0, 0);")
-    L.append("      }")
+    if PAIRS:
+        # x pairs then g pairs, each a pointer stepping by 2 pairs (4 rows); pads only at the end
+        for (arr, P0, P1, DD, off) in (("xr", 0, PX, D, 0), ("gr", PX, PX + PG, Dout, PX)):
+            L.append(f"      {{ int pp = {P0} + ((h - {P0}) & 1);          // the first pair >= {P0} of this wave's parity")
+            L.append(f"        const float* sp = {arr} + (size_t)(2 * (pp - {off})) * n_nodes + n0;")
+            L.append(f"        for (; pp < {P1}; pp += 2, sp += (size_t)4 * n_nodes, ++k) {{")
+            last_pad = DD % 2 == 1
+            lo = f"(pp == {P1 - 1} ? lo1 : lo2)" if last_pad else "lo2"
+            L.append(f"          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(sp + {lo}),")
+            L.append(f"              (__attribute__((address_space(3))) void*)(dst + pp * {SC * 2} + nbk * 64), 4, 0, 0);")
+            L.append("        }")
+            L.append("      }")
+    else:
+        L.append(f"      for (int row = wv; row < {ROWS}; row += {WV}, ++k) {{   // wave-uniform")
+        L.append(f"        const float* src = (row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes) + n0 + lane * 4;")
+        L.append("        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,")
+        L.append(f"            (__attribute__((address_space(3))) void*)(dst + row * {SC}), 16, 0, 0);")
+    if not PAIRS:
+        L.append("      }")
     L.append("      return k;")
     L.append("    } else {")
-    L.append(f"      for (int i = threadIdx.x; i < {ROWS * SC}; i += {64 * WV}) {{")
-    L.append(f"        const int row = i / {SC}, j = i - row * {SC}, n = n0 + j;")
-    L.append(f"        const float* src = row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes;")
-    L.append("        dst[i] = n < nb1 ? src[n] : 0.0f;")
+    L.append(f"      for (int i = threadIdx.x; i < {BUFF}; i += {64 * WV}) {{")
+    if PAIRS:
+        L.append(f"        const int pp = i / {2 * SC}, j = (i - pp * {2 * SC}) >> 1, n = n0 + j;")
+        L.append(f"        const bool isx = pp < {PX};")
+        L.append(f"        const int row = 2 * (isx ? pp : pp - {PX}) + (i & 1);")
+        L.append(f"        const bool ok = n < nb1 && row < (isx ? {D} : {Dout});")
+        L.append("        dst[i] = ok ? (isx ? xr : gr)[(size_t)row * n_nodes + n] : 0.0f;")
+    else:
+        L.append(f"        const int row = i / {SC}, j = i - row * {SC}, n = n0 + j;")
+        L.append(f"        const float* src = row < {D} ? xr + (size_t)row * n_nodes : gr + (size_t)(row - {D}) * n_nodes;")
+        L.append("        dst[i] = n < nb1 ? src[n] : 0.0f;")
     L.append("      }")
     L.append('      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // stores done before the barrier')
     L.append("      return 0;")
@@ -1985,13 +2041,14 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     # the chunk loop sits inside each case: the accumulators never meet at a merge point inside
     # the loop (a switch inside the loop made the compiler move all 64 of them at every case exit
     # and spill); every wave, a group-less one too, runs the same stages and barriers
+    lane_b = 8 if PAIRS else 4
     head = ["      int b = 0;",
             f"      for (int n0 = nb0; n0 < nb1; n0 += {SC}, b = b == {NBUF - 1} ? 0 : b + 1) {{",
             "        retire(pend);                         // chunk n0 landed (this wave's part)",
             '        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");',
             "        __builtin_amdgcn_s_barrier();        // every wave's part; the buffer restaged next is free",
             f"        pend = stage(b == 0 ? 2 : b - 1, n0 + {2 * SC});",
-            f"        const unsigned ab = lds0 + b * {ROWS * RB} + lane * 4;"]
+            f"        const unsigned ab = lds0 + b * {BUFF * 4} + lane * {lane_b};"]
     tail = ["      }",
             '      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");']
     L.append("  switch (jg) {")
@@ -2000,23 +2057,10 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
             continue
         L.append(f"    case {gi}: {{")
         L += head
-        need_x, need_g = set(), set()
-        for t in grp:
-            nu, (a, b_, cc), qq = plan.terms[t]
-            need_g.add(qq)
-            need_x.add(a)
-            if nu >= 2:
-                need_x.add(b_)
-            if nu >= 3:
-                need_x.add(cc)
-        ops = [("x", a, a) for a in sorted(need_x)] + [("g", qq, D + qq) for qq in sorted(need_g)]
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         L.append("#pragma unroll 1")
         L.append(f"      for (int sb = 0; sb < {SC // 64}; ++sb) {{")
-        L.append("        const unsigned a_ = ab + sb * 256;")
-        # operand reads: pairs of rows by ds_read2st64_b32 (offsets in 256-B units), in the
-        # order the terms first use them; each operand is waited for (counted lgkmcnt) just
-        # before its first use, so the FMAs start while the later reads are in flight
+        L.append(f"        const unsigned a_ = ab + sb * {64 * lane_b};")
         order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
         seq = []
         for jj in order:
@@ -2025,12 +2069,28 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
                       [("x", a), ("x", b_)] + ([("x", cc)] if nu == 3 else []) + [("g", qq)]):
                 if o not in seq:
                     seq.append(o)
-        row = {("x", a): a for a in need_x} | {("g", qq): D + qq for qq in need_g}
-        reads = [seq[k: k + 2] for k in range(0, len(seq), 2)]
-        ridx = {o: k for k, rd in enumerate(reads) for o in rd}
+        if PAIRS:
+            # a read = one row pair: (kind, pair) in first-use order; it yields both rows
+            def pair_of(o):
+                return (o[0], o[1] // 2)
+            reads = []
+            for o in seq:
+                if pair_of(o) not in reads:
+                    reads.append(pair_of(o))
+            ridx = {o: reads.index(pair_of(o)) for o in seq}
+            used = set(seq)
+        else:
+            reads = [tuple(seq[k: k + 2]) for k in range(0, len(seq), 2)]
+            ridx = {o: k for k, rd in enumerate(reads) for o in rd}
+        row = {o: (o[1] if o[0] == "x" else D + o[1]) for o in seq}
         L.append("        float " + ", ".join(f"{o[0]}{o[1]}" for o in seq) + ";")
         for k, rd in enumerate(reads):
-            if len(rd) == 2:
+            if PAIRS:
+                kind, pp = rd
+                blk = pp if kind == "x" else PX + pp
+                L.append(f"        eelg_f2r p{k};")
+                L.append(f'        asm volatile("ds_read_b64 %0, %1 offset:{blk * PB}" : "=v"(p{k}) : "v"(a_));')
+            elif len(rd) == 2:
                 L.append(f"        eelg_f2r p{k};")
                 L.append(f'        asm volatile("ds_read2st64_b32 %0, %1 offset0:{row[rd[0]] * (RB // 256)} '
                          f'offset1:{row[rd[1]] * (RB // 256)}" : "=v"(p{k}) : "v"(a_));')
@@ -2044,11 +2104,16 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
             if k <= state["w"]:
                 return
             regs = [f"p{j}" for j in range(state["w"] + 1, k + 1)]
-            L.append(f'        asm volatile("s_waitcnt lgkmcnt({len(reads) - 1 - k})" : ' +
+            # (the counter field holds 0..15: a larger count waits for more than this read)
+            L.append(f'        asm volatile("s_waitcnt lgkmcnt({min(15, len(reads) - 1 - k)})" : ' +
                      ", ".join(f'"+v"({v})' for v in regs) + ' : : "memory");')
             for j in range(state["w"] + 1, k + 1):
                 rd = reads[j]
-                if len(rd) == 2:
+                if PAIRS:
+                    kind, pp = rd
+                    parts = [f"{kind}{2 * pp + h} = p{j}[{h}];" for h in (0, 1) if (kind, 2 * pp + h) in used]
+                    L.append("        " + " ".join(parts))
+                elif len(rd) == 2:
                     L.append(f"        {rd[0][0]}{rd[0][1]} = p{j}[0]; {rd[1][0]}{rd[1][1]} = p{j}[1];")
                 else:
                     L.append(f"        {rd[0][0]}{rd[0][1]} = p{j};")
