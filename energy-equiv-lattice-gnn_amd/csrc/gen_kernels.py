@@ -134,6 +134,14 @@ SC_COEF_SC = 256                      # nodes per streamed chunk: one 1-KiB LDS-
 # LDS-DMA instructions per chunk instead of 50 sixteen-byte ones, SALU 55 -> 88 M, issue
 # stalls 186 -> 260 M per launch) -- the halved LDS read cycles do not pay for the fill
 SC_COEF_PAIRS = int(os.environ.get("EELG_SC_COEF_PAIRS", "0"))
+# packed streaming coefficient gradient: two nodes per lane (a ds_read_b64 of two consecutive
+# nodes of a row), v_pk_mul_f32 / v_pk_fma_f32 on node pairs, <= SC_COEF_PK_JG terms per group
+# (two accumulator registers per term).  Measured (r08i, kbench): 0.500-0.506 vs 0.410 ms
+# unpacked -- VALU instructions 208 -> 129 M per launch, but the 32-term groups need 15 sets
+# of workgroups per tile (twice the chunk staging) and a step's compute shrinks 3.5x against a
+# fixed staging and barrier cost (SQ_WAIT_ANY 42 %), so it stays off
+SC_COEF_PK = int(os.environ.get("EELG_SC_COEF_PK", "0"))
+SC_COEF_PK_JG = int(os.environ.get("EELG_SC_COEF_PK_JG", "32"))
 # Variants built, measured slower and removed (DESIGN.md section 3 records the numbers): packed
 # channel-pair TP forward, 2x-unrolled TP edge loop, shared-coupling (M in LDS) and cooperative
 # TP forwards, two nodes / two channels per lane in the contraction, mul-major coefficient
@@ -1895,16 +1903,18 @@ def emit_sc(name: str, coupling: str, ls: Tuple[int, ...], corr: int) -> Tuple[s
     L.append("}")
     WPB, NBC = WV, NCB
     cstream = 0
+    csets = 0
     if SC_COEF_STREAM:
-        L += emit_sc_coef_stream(name, plan, D, Dout, cld)
+        code, csets = emit_sc_coef_stream(name, plan, D, Dout, cld)
+        L += code
         cstream, NBC = 1, SC_COEF_SC
     info = dict(D=D, Dout=Dout, drow=drow, orow=orow, nterms=nt, cld=cld, njg=len(groups), wpb=WPB, nbc=NBC, nb=NB, nth=NTH,
-                cmajor_out=cmajor_out, cstream=cstream, csets=-(-nt // (16 * SC_COEF_MAXJG)),
+                cmajor_out=cmajor_out, cstream=cstream, csets=csets,
                 sig=fnv1a64(sc_signature(coupling, ls, corr)))
     return "\n".join(L), info
 
 
-def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[str]:
+def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> Tuple[List[str], int]:
     """Streaming coefficient gradient ``sc_bwd_coefs_<name>`` (round 6).
 
     grad coef[c, t] = sum_n g_q(n) x_a(n) x_b(n) x_c(n) over the channel-major rows
@@ -1931,10 +1941,11 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     deterministic partial per range."""
     WV, SC = 16, SC_COEF_SC
     PAIRS = SC_COEF_PAIRS
+    PK = SC_COEF_PK and not PAIRS
     nt = len(plan.terms)
-    S = -(-nt // (WV * SC_COEF_MAXJG))
+    S = -(-nt // (WV * (SC_COEF_PK_JG if PK else SC_COEF_MAXJG)))
     JG = -(-nt // (WV * S))
-    assert JG <= 64
+    assert JG <= (32 if PK else 64)
     groups = coef_sets(plan, S, WV, JG)
     ROWS = D + Dout
     NBUF = 3
@@ -1955,7 +1966,7 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     perm = [(grp[j] if j < len(grp) else -1) for grp in groups for j in range(64)]
     L: List[str] = []
     L.append(f"// streaming coefficient gradient: {S} sets x {WV} term groups of <= {JG} terms, "
-             f"{SC}-node chunks, {'row-pair' if PAIRS else 'row'} image")
+             f"{SC}-node chunks, {'row-pair' if PAIRS else 'row'} image{', two nodes per lane' if PK else ''}")
     L.append(f"__device__ const short sc_coefs_perm_{name}[{len(perm)}] = {{")
     for k in range(0, len(perm), 32):
         L.append("  " + ", ".join(str(v) for v in perm[k: k + 32]) + ",")
@@ -2033,15 +2044,21 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
         L.append(f'    {"if" if k == NW else "else if"} (p >= {k}) asm volatile("s_waitcnt vmcnt({k})" ::: "memory");')
     L.append('    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
     L.append("  };")
-    L.append("  float acc[64];")
-    L.append("#pragma unroll")
-    L.append("  for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
+    if PK:
+        L.append(f"  eelg_f2r acc[{JG}];")
+        L.append("#pragma unroll")
+        L.append(f"  for (int i = 0; i < {JG}; ++i) acc[i] = (eelg_f2r){{0.0f, 0.0f}};")
+    else:
+        L.append("  float acc[64];")
+        L.append("#pragma unroll")
+        L.append("  for (int i = 0; i < 64; ++i) acc[i] = 0.0f;")
     L.append("  stage(0, nb0);")
     L.append(f"  int pend = stage(1, nb0 + {SC});           // this wave's DMAs of the chunk after the current")
     # the chunk loop sits inside each case: the accumulators never meet at a merge point inside
     # the loop (a switch inside the loop made the compiler move all 64 of them at every case exit
     # and spill); every wave, a group-less one too, runs the same stages and barriers
-    lane_b = 8 if PAIRS else 4
+    lane_b = 8 if (PAIRS or PK) else 4       # bytes per lane of a sub-tile row read
+    NST = 128 if PK else 64                  # nodes per sub-tile
     head = ["      int b = 0;",
             f"      for (int n0 = nb0; n0 < nb1; n0 += {SC}, b = b == {NBUF - 1} ? 0 : b + 1) {{",
             "        retire(pend);                         // chunk n0 landed (this wave's part)",
@@ -2059,7 +2076,7 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
         L += head
         cpin = pin([f"acc[{jj}]" for jj in range(len(grp))])
         L.append("#pragma unroll 1")
-        L.append(f"      for (int sb = 0; sb < {SC // 64}; ++sb) {{")
+        L.append(f"      for (int sb = 0; sb < {SC // NST}; ++sb) {{")
         L.append(f"        const unsigned a_ = ab + sb * {64 * lane_b};")
         order = sorted(range(len(grp)), key=lambda jj: (plan.terms[grp[jj]][0] > 1,) + plan.terms[grp[jj]][1])
         seq = []
@@ -2079,17 +2096,24 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
                     reads.append(pair_of(o))
             ridx = {o: reads.index(pair_of(o)) for o in seq}
             used = set(seq)
+        elif PK:
+            reads = [(o,) for o in seq]           # one row per read, two nodes
+            ridx = {o: k for k, rd in enumerate(reads) for o in rd}
         else:
             reads = [tuple(seq[k: k + 2]) for k in range(0, len(seq), 2)]
             ridx = {o: k for k, rd in enumerate(reads) for o in rd}
         row = {o: (o[1] if o[0] == "x" else D + o[1]) for o in seq}
-        L.append("        float " + ", ".join(f"{o[0]}{o[1]}" for o in seq) + ";")
+        VT = "eelg_f2r" if PK else "float"
+        L.append(f"        {VT} " + ", ".join(f"{o[0]}{o[1]}" for o in seq) + ";")
         for k, rd in enumerate(reads):
             if PAIRS:
                 kind, pp = rd
                 blk = pp if kind == "x" else PX + pp
                 L.append(f"        eelg_f2r p{k};")
                 L.append(f'        asm volatile("ds_read_b64 %0, %1 offset:{blk * PB}" : "=v"(p{k}) : "v"(a_));')
+            elif PK:
+                L.append(f"        eelg_f2r p{k};")
+                L.append(f'        asm volatile("ds_read_b64 %0, %1 offset:{row[rd[0]] * RB}" : "=v"(p{k}) : "v"(a_));')
             elif len(rd) == 2:
                 L.append(f"        eelg_f2r p{k};")
                 L.append(f'        asm volatile("ds_read2st64_b32 %0, %1 offset0:{row[rd[0]] * (RB // 256)} '
@@ -2113,6 +2137,8 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
                     kind, pp = rd
                     parts = [f"{kind}{2 * pp + h} = p{j}[{h}];" for h in (0, 1) if (kind, 2 * pp + h) in used]
                     L.append("        " + " ".join(parts))
+                elif PK:
+                    L.append(f"        {rd[0][0]}{rd[0][1]} = p{j};")
                 elif len(rd) == 2:
                     L.append(f"        {rd[0][0]}{rd[0][1]} = p{j}[0]; {rd[1][0]}{rd[1][1]} = p{j}[1];")
                 else:
@@ -2122,27 +2148,29 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
         for jj in order:
             t = grp[jj]
             nu, (a, b_, cc), qq = plan.terms[t]
+            FMA = (lambda u, v, w: f"__builtin_elementwise_fma({u}, {v}, {w})") if PK else \
+                (lambda u, v, w: f"fmaf({u}, {v}, {w})")
             if nu == 1:
                 need(("x", a), ("g", qq))
-                L.append(f"        acc[{jj}] = fmaf(x{a}, g{qq}, acc[{jj}]);")
+                L.append(f"        acc[{jj}] = {FMA(f'x{a}', f'g{qq}', f'acc[{jj}]')};")
                 continue
             if cur != (a, b_):
                 if cur is not None:
                     L.append("        }")
                     L.append("        " + cpin)
                 need(("x", a), ("x", b_))
-                L.append(f"        {{ const float pp = x{a} * x{b_};")
+                L.append(f"        {{ const {VT} pp = x{a} * x{b_};")
                 cur, curc = (a, b_), None
             if nu == 2:
                 need(("g", qq))
-                L.append(f"          acc[{jj}] = fmaf(pp, g{qq}, acc[{jj}]);")
+                L.append(f"          acc[{jj}] = {FMA('pp', f'g{qq}', f'acc[{jj}]')};")
             else:
                 if curc != cc:
                     need(("x", cc))
-                    L.append(f"          const float m{cc} = pp * x{cc};")
+                    L.append(f"          const {VT} m{cc} = pp * x{cc};")
                     curc = cc
                 need(("g", qq))
-                L.append(f"          acc[{jj}] = fmaf(m{cc}, g{qq}, acc[{jj}]);")
+                L.append(f"          acc[{jj}] = {FMA(f'm{cc}', f'g{qq}', f'acc[{jj}]')};")
         if cur is not None:
             L.append("        }")
         L.append("        " + cpin)
@@ -2153,11 +2181,20 @@ def emit_sc_coef_stream(name: str, plan, D: int, Dout: int, cld: int) -> List[st
     L += [ln for ln in head if "const unsigned ab" not in ln] + tail
     L.append("      break; }")
     L.append("  }")
-    L.append("  eelg_lane_reduce64(acc);")
-    L.append(f"  const int t = sc_coefs_perm_{name}[jg * 64 + lane];")
-    L.append(f"  if (t >= 0) part[((size_t)r * {MUL} + c) * {cld} + t] = acc[0];")
+    if PK:
+        # the two nodes of each lane first, then the 64 lanes
+        L.append("  float red[64];")
+        L.append("#pragma unroll")
+        L.append(f"  for (int i = 0; i < 64; ++i) red[i] = i < {JG} ? acc[i < {JG} ? i : 0][0] + acc[i < {JG} ? i : 0][1] : 0.0f;")
+        L.append("  eelg_lane_reduce64(red);")
+        L.append(f"  const int t = sc_coefs_perm_{name}[jg * 64 + lane];")
+        L.append(f"  if (t >= 0) part[((size_t)r * {MUL} + c) * {cld} + t] = red[0];")
+    else:
+        L.append("  eelg_lane_reduce64(acc);")
+        L.append(f"  const int t = sc_coefs_perm_{name}[jg * 64 + lane];")
+        L.append(f"  if (t >= 0) part[((size_t)r * {MUL} + c) * {cld} + t] = acc[0];")
     L.append("}")
-    return L
+    return L, S
 
 
 # ---------------------------------------------------------------------------

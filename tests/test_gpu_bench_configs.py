@@ -54,4 +54,7 @@ def test_bench_config5_bf16_storage():
     assert math.isfinite(out["value"]) and out["value"] > 0 and math.isfinite(out["loss"])
     roof = out["roofline"]
     assert roof is not None and roof["kernel"].startswith("tp_fwd_tpB_l3")
-    assert roof["launches"] == 2 * 3                                   # layers 1..3 per step
+    # frac from the 5 in-line steps after the timed region (bench --inline-steps), layers 1..3;
+    # the overlapped timed region's own figure beside it (2 timed steps)
+    assert roof["launches"] == 5 * 3 and roof["overlapped"]["launches"] == 2 * 3
+    assert 0 < roof["frac"] < 1.5 and 0 < roof["overlapped"]["frac"] < 1.5
