@@ -889,12 +889,16 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
   return check_launch("sc_cmajor");
 }
 
-// streaming coefficient gradient: the nodes are split into at most 4 ranges (one partial row
-// each) of whole chunks, so that 32 channels x 4 ranges x the term-group sets fill the chip
-// several times over without a workgroup per chunk
-static int sc_coef_range(const eelg_sc_cfg& c, int n_nodes) {
-  int nr = (n_nodes + 8191) / 8192;
-  nr = nr < 1 ? 1 : (nr > 4 ? 4 : nr);
+// streaming coefficient gradient: the nodes are split into node ranges (one partial row each)
+// of whole chunks, so that mul channels x ranges x the term-group sets make about four rounds
+// of one-workgroup-per-CU blocks on the 256 CUs (lmax 4, correlation 3: 4 ranges; lmax 3:
+// 16), with ranges of at least 2048 nodes
+static int sc_coef_range(const eelg_sc_cfg& c, int n_nodes, int mul) {
+  const int per = mul * (c.csets > 0 ? c.csets : 1);
+  int nr = (1024 + per - 1) / per;
+  const int nmax = (n_nodes + 2047) / 2048;
+  nr = nr > nmax ? nmax : nr;
+  nr = nr < 1 ? 1 : nr;
   const int rn = (n_nodes + nr - 1) / nr;
   return (rn + c.nbc - 1) / c.nbc * c.nbc;
 }
@@ -903,7 +907,7 @@ int eelg_sc_bwd_coef_parts(int cfg, int n_nodes, int mul) {
   const eelg_sc_cfg* c = sc_get(cfg, mul);
   if (!c) return -1;
   if (n_nodes <= 0) return 0;
-  const int rn = c->bwd_coefs ? sc_coef_range(*c, n_nodes) : c->nbc;
+  const int rn = c->bwd_coefs ? sc_coef_range(*c, n_nodes, mul) : c->nbc;
   return (n_nodes + rn - 1) / rn;
 }
 
@@ -917,7 +921,7 @@ int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes, int
   if (n_nodes <= 0) return 0;
   if (c->bwd_coefs) {
     // one workgroup per (channel x node range tile, term-group set); partial[range, channel, t]
-    const int rn = sc_coef_range(*c, n_nodes);
+    const int rn = sc_coef_range(*c, n_nodes, mul);
     const int tiles = mul * ((n_nodes + rn - 1) / rn);
     hipLaunchKernelGGL(c->bwd_coefs, dim3(((tiles + 7) / 8) * 8 * c->csets), dim3(1024), 0,
                        (hipStream_t)stream, xt, gt, n_nodes, rn, partial);

@@ -238,8 +238,9 @@ int eelg_sc_cmajor(int cfg, int which, const float* x, int n_nodes, int mul, flo
  * gnn/mace.py:242-277) from the channel-major copies xt[(c*D + a)*N + n] / gt of x and
  * grad_out (eelg_sc_bwd_x_cm or eelg_sc_cmajor).  partial[n_parts, mul, coef_ld] (the
  * entries past nterms of each row are not written), n_parts = eelg_sc_bwd_coef_parts(cfg,
- * n_nodes, mul): one partial per node range (streaming kernel: at most 4 ranges of whole
- * coef_chunk-node chunks; round-5 chunk kernel: one per coef_chunk nodes).  chunk must be the
+ * n_nodes, mul): one partial per node range (streaming kernel: ranges of whole coef_chunk-node
+ * chunks, about 1024 / (mul x term-group sets) of them and at least 2048 nodes each; round-5
+ * chunk kernel: one per coef_chunk nodes).  chunk must be the
  * config's coef_chunk (info[6]).  The caller sums over the partials (deterministic).
  * Non-overlapping xt / gt; 16-byte aligned rows (n_nodes % 4 == 0) take the LDS-DMA path. */
 int eelg_sc_bwd_coef(int cfg, const float* xt, const float* gt, int n_nodes,
