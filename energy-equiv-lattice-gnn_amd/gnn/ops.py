@@ -60,17 +60,19 @@ SC_COEF_ON_SIDE = os.environ.get("EELG_SC_COEF_SIDE", "1") != "0"
 # or the fused small-layer kernel with per-workgroup partials (0)
 RADIAL_CHAIN = os.environ.get("EELG_RADIAL_CHAIN", "1") != "0"
 # TP backward in sender order (eelg_tp_bwd_sender) instead of per-edge gxe + sender segment sum:
-# "1" always, "0" never, "auto" (default) for bf16 storage only.  fp32: measured slower (r02s1:
+# "1" always, "0" never (default), "auto" for bf16 storage only.  fp32: measured slower (r02s1:
 # tp_bws 1.40 ms vs tp_bwd 1.05 + sender sum 0.16 ms; 1832 vs 1862 graphs/s) -- each edge
 # gathers its receiver's 29 KB grad_agg row out of receiver order.  bf16 storage (config 5):
-# equal speed (r02s2: 912.1 vs 912.4 graphs/s) and grad_x is summed in fp32 instead of from
-# per-edge terms rounded to bf16.
+# equal speed in round 2 (r02s2: 912.1 vs 912.4 graphs/s), so "auto" was the default, summing
+# grad_x in fp32 instead of from per-edge terms rounded to bf16; with round 3-6's edge kernel
+# (deeper prefetch, XCD-ordered blocks) the edge path is faster (r08m, two alternating pairs:
+# 1145.6 / 1143.7 vs 1130.0 / 1127.9 graphs/s; tp_bwd 1.90 vs tp_bws 2.23 ms per launch)
 # edge-order backward: gxe rows stored at their sender-order position (eelg_tp_bwd_sorted), so
 # the sender sum reads them contiguously instead of gathering through sperm.  Bitwise-equal
 # results; measured equal (r02s3: sender sum 169 -> 137 us, tp_bwd 1036 -> 1128 us from the
 # scattered row stores; 1844 / 1855 vs 1844 / 1847 graphs/s), so off by default.
 TP_BWD_SPOS = os.environ.get("EELG_TP_BWD_SPOS", "0") != "0"
-_TBS = os.environ.get("EELG_TP_BWD_SENDER", "auto")
+_TBS = os.environ.get("EELG_TP_BWD_SENDER", "0")
 TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
