@@ -608,6 +608,54 @@ int eelg_tp_bwd_bf16(int cfg, const float* x, const float* sh, const void* w, co
                                  inv_norm, grad_w, gxe, stream);
 }
 
+// fused output-linear grad-x + backward: R-receiver tiles x nbgroups input blocks, 1-D grid with
+// the tiles rounded up to a multiple of 8 (the group blocks of a tile share an XCD; gen_kernels.py)
+static dim3 tp_bwf_grid(const eelg_tp_cfg& c, int n_nodes) {
+  const int nt = (n_nodes + c.bwf_r - 1) / c.bwf_r;
+  return dim3(((nt + 7) / 8) * 8 * c.nbgroups);
+}
+
+int eelg_tp_bwf_slot(int cfg, int slot, int* w_off, float* alpha, int* gy_off) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (!c->bwf) return fail(-2, "tp_bwd_fused: not generated for config %s (mul 32 only)", c->name);
+  if (slot < 0 || slot >= c->npaths) return fail(-3, "tp_bwf_slot: slot %d of %d", slot, c->npaths);
+  *w_off = c->bwf_slots[slot][0];
+  *gy_off = c->bwf_slots[slot][1];
+  *alpha = c->bwf_alpha[slot];
+  return 0;
+}
+
+int eelg_tp_bwd_fused(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                      const int* receiver,
+                      const int* rowptr, int n_nodes, const float* gy, const float* lin_w,
+                      float inv_norm, float* grad_w, float* gxe, void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (!c->bwf) return fail(-2, "tp_bwd_fused: not generated for config %s (mul 32 only)", c->name);
+  if (reinterpret_cast<uintptr_t>(lin_w) & 15) return fail(-3, "tp_bwd_fused: linear weight not 16-B aligned");
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->bwf, tp_bwf_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x, sh, w,
+                     sender, receiver, rowptr, n_nodes, gy, lin_w, inv_norm, grad_w, gxe);
+  return check_launch("tp_bwd_fused");
+}
+
+int eelg_tp_bwd_fused_bf16(int cfg, const float* x, const float* sh, const void* w,
+                           const int* sender, const int* receiver, const int* rowptr,
+                           int n_nodes, const float* gy,
+                           const float* lin_w, float inv_norm, void* grad_w, void* gxe,
+                           void* stream) {
+  const eelg_tp_cfg* c = tp_cfg(cfg);
+  if (!c) return -1;
+  if (!c->bwf_bf) return fail(-2, "tp_bwd_fused_bf16: not generated for config %s", c->name);
+  if (reinterpret_cast<uintptr_t>(lin_w) & 15) return fail(-3, "tp_bwd_fused: linear weight not 16-B aligned");
+  if (n_nodes <= 0) return 0;
+  hipLaunchKernelGGL(c->bwf_bf, tp_bwf_grid(*c, n_nodes), dim3(256), 0, (hipStream_t)stream, x, sh,
+                     static_cast<const unsigned short*>(w), sender, receiver, rowptr, n_nodes, gy, lin_w,
+                     inv_norm, static_cast<unsigned short*>(grad_w), static_cast<unsigned short*>(gxe));
+  return check_launch("tp_bwd_fused_bf16");
+}
+
 // one half-wave per sender node, nbgroups input blocks on blockIdx.y
 int eelg_tp_bwd_sender(int cfg, const float* x, const float* sh, const float* w, const int* sperm,
                        const int* srowptr, const int* receiver, int n_nodes,

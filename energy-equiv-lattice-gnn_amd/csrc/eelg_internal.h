@@ -20,6 +20,18 @@ typedef void (*eelg_tp_bws_fn)(const float*, const float*, const float*, const i
 typedef void (*eelg_tp_bws_bf_fn)(const float*, const float*, const unsigned short*, const int*,
                                   const int*, const int*, int, const float*, float,
                                   unsigned short*, float*);
+// fused output-linear grad-x + backward: (x, sh, w, sender, receiver, rowptr, n_nodes, gy,
+// linear weight, inv_norm, grad_w, gxe)
+typedef void (*eelg_tp_bwf_fn)(const float*, const float*, const float*, const int*, const int*,
+                               const int*, int, const float*, const float*, float, float*, float*);
+typedef void (*eelg_tp_bwf_bf_fn)(const float*, const float*, const unsigned short*, const int*,
+                                  const int*, const int*, int, const float*, const float*, float,
+                                  unsigned short*, unsigned short*);
+// one MFMA task of tp_bwf's grad_agg stage: a 32-column tile (ct) of one slot's [32 x R*d3] block
+struct eelg_bwf_task {
+  int d3, ct, lds, woff, gyoff;
+  float alpha;
+};
 typedef void (*eelg_sc_fwd_fn)(const float*, const float*, int, float*);
 typedef void (*eelg_sc_bwdx_fn)(const float*, const float*, const float*, int, float*, float*,
                                 float*);
@@ -41,6 +53,12 @@ struct eelg_tp_cfg {
   eelg_tp_bws_bf_fn bws_bf;
   int ngroups_bf;            // path groups of the bf16-weight forward (its own accumulator cap)
   int bxcd;                  // tp_bwd block placement (gen_kernels.TP_BWD_XCD): 0 = 2-D grid, else 1-D XCD ranges
+  eelg_tp_bwf_fn bwf;        // fused output-linear grad-x + backward (nullptr: not generated)
+  eelg_tp_bwf_bf_fn bwf_bf;
+  int bwf_r;                 // its receivers per workgroup
+  int tdim;                  // the output linear's row (target irreps dim)
+  const int (*bwf_slots)[2]; // per slot: linear weight offset, gy offset
+  const float* bwf_alpha;    // per slot: the linear's alpha
 };
 
 struct eelg_sc_cfg {

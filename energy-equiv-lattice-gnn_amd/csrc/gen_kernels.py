@@ -79,6 +79,17 @@ TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "1"))
 # With 0 a receiver whose in-edges straddle two blocks has its grad_agg row fetched into two
 # L2s, and every XCD gathers every lattice's x rows
 TP_BWD_XCD = int(os.environ.get("EELG_TP_BWD_XCD", "2"))
+# fused output-linear grad-x + TP backward (tp_bwf, mul 32; off by default, gnn/ops.py TP_BWF):
+# receivers per workgroup whose [Σ d3 × 32] grad_agg block of one input-block group is computed
+# by MFMA into LDS from the linear's output gradient, then read by the tile's in-edges.
+# r09c kbench (tp_bwd 0.682 + linear grad-x 0.324 ms unfused): R 8 receiver-major 1.417 ms,
+# edge-major 1.242, edge-major without the next-edge prefetch 1.142, the same at R 4 1.104;
+# the MFMA stage alone (R 8) 0.505 ms -- latency-bound at 2 waves / SIMD (LDS and VGPRs)
+TP_BWF_R = int(os.environ.get("EELG_TP_BWF_R", "4"))
+TP_BWF_SKIP = int(os.environ.get("EELG_TP_BWF_SKIP", "0"))   # measurement only: 1 = no edge stage, 2 = no MFMA stage
+TP_BWF_EM = int(os.environ.get("EELG_TP_BWF_EM", "1"))       # edge stage: 1 = the tile's edges dealt over the half-waves
+TP_BWF_NX = int(os.environ.get("EELG_TP_BWF_NX", "0"))       # edge stage: next edge's x / SH / weight loads one edge ahead
+TP_BWF_P1PF = int(os.environ.get("EELG_TP_BWF_P1PF", "1"))   # MFMA stage: next task's operands loaded one task ahead
 # symmetric contraction: coefficient blocks (32 terms each) in flight ahead of the block being
 # computed, and the terms per block, forward / grad-x (r03r/r03s, grad-x: 32 terms 2 ahead
 # 0.407 ms, 64 terms 1 ahead 0.363 ms; 16 terms 3-4 ahead 0.57 ms; the forward: 32 or 40 terms
@@ -599,6 +610,244 @@ def _emit_tp_fwd_glds2(name, groups, din, nshp, dmid, wn, node_off, bf: bool = F
     return L
 
 
+def bwf_slot_table(paths, target: Irreps) -> Dict[int, Tuple[int, float, int]]:
+    """slot -> (weight offset of its 32 x 32 block, alpha, gy offset) in the output linear
+    ``o3.Linear(irreps_mid.simplify(), target)``: irreps_mid is sorted by l3, so the slots of
+    one l3 form one merged input block (mul 32 x their count), whose instruction's weight is
+    [32·cnt, 32] row-major with alpha 1/sqrt(32·cnt); instructions run in l3 order.  The host
+    checks this table against the Linear it is handed (``eelg_tp_bwf_slot``)."""
+    cnt: Dict[int, int] = {}
+    for p in paths:
+        cnt[p.l3] = cnt.get(p.l3, 0) + 1
+    woff, o = {}, 0
+    for l3 in sorted(cnt):
+        woff[l3] = o
+        o += 32 * cnt[l3] * MUL
+    tgt_off = {ir.l: off for (m, ir), off in zip(target, target.offsets())}
+    seen: Dict[int, int] = {}
+    tab = {}
+    for p in sorted(paths, key=lambda p: p.slot):
+        q = seen.get(p.l3, 0)
+        seen[p.l3] = q + 1
+        tab[p.slot] = (woff[p.l3] + q * 32 * MUL, 1.0 / math.sqrt(32 * cnt[p.l3]), tgt_off[p.l3])
+    return tab
+
+
+def _emit_tp_bwf(name, sfx, bgroups, paths, target, din, nshp, wn, node_off, bf, ld_w, st_w):
+    """Fused backward of ``linear(tp_interaction(x, sh, w))`` w.r.t. x and w, from the linear's
+    output gradient gy [N, target.dim] (mul 32).  A workgroup owns R receivers and one input
+    block l1 (grid: tiles x groups, the groups of a tile on one XCD):
+      1. grad_agg of the group's slots for the R receivers, G[r][s][u][m] =
+         alpha(l3) Σ_j W_s[u][j] gy[r][off(l3) + j·d3 + m], on v_mfma_f32_32x32x2f32 (rows u,
+         columns (r, m), K = j) into LDS -- the [N, dmid] grad_agg tensor of the unfused path
+         (written by the linear's grad-x, read back by tp_bwd) never reaches HBM;
+      2. each half-wave streams the in-edges of one receiver (receiver-sorted order: one
+         contiguous range) with tp_bwd's per-path arithmetic, its grad_agg slices read from LDS,
+         storing grad_w and the per-edge grad_x rows (gxe) as tp_bwd does."""
+    WT = "unsigned short" if bf else "float"
+    R = TP_BWF_R
+    tab = bwf_slot_table(paths, target)
+    tdim = target.dim
+    L: List[str] = []
+    tasks, tb, sgs, lds_of = [], [0], [], {}
+    for grp in bgroups:
+        off = 0
+        for p in grp:
+            d3 = 2 * p.l3 + 1
+            lds_of[p.slot] = off
+            wo, al, go = tab[p.slot]
+            for ct in range((R * d3 + 31) // 32):
+                tasks.append((d3, ct, off, wo, go, al))
+            off += 32 * d3
+        sgs.append(off)
+        tb.append(len(tasks))
+    sgmax = max(sgs)
+    nbg = len(bgroups)
+    tn = f"bwf_tasks_{name}"
+    if not bf:   # one task table per structure (shared by the bf16-storage kernel)
+        L.append(f"static __constant__ eelg_bwf_task {tn}[{len(tasks)}] = {{")
+        L += [f"  {{{d3}, {ct}, {off}, {wo}, {go}, {flit(al)}}}," for d3, ct, off, wo, go, al in tasks]
+        L.append("};")
+        L.append(f"static __constant__ int bwf_tb_{name}[{nbg + 1}] = {{{', '.join(map(str, tb))}}};")
+        L.append(f"static __constant__ int bwf_sg_{name}[{nbg}] = {{{', '.join(map(str, sgs))}}};")
+        L.append(f"static const int bwf_slots_{name}[{len(paths)}][2] = {{"
+                 + ", ".join(f"{{{tab[s][0]}, {tab[s][2]}}}" for s in sorted(tab)) + "};")
+        L.append(f"static const float bwf_alpha_{name}[{len(paths)}] = {{"
+                 + ", ".join(flit(tab[s][1]) for s in sorted(tab)) + "};")
+    EM, NX, P1 = TP_BWF_EM, TP_BWF_NX, TP_BWF_P1PF
+    L.append(f"__global__ __launch_bounds__(256) void tp_bwf_{name}{sfx}(")
+    L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
+    L.append("    const int* __restrict__ sender, const int* __restrict__ receiver,")
+    L.append("    const int* __restrict__ rowptr, int n_nodes,")
+    L.append("    const float* __restrict__ gy, const float* __restrict__ wl, float inv_norm,")
+    L.append(f"    {WT}* __restrict__ gw, {WT}* __restrict__ gxe) {{")
+    L.append(f"  __shared__ float Gs[{R * sgmax}];")
+    L.append("  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane & 31, hf = lane >> 5;")
+    # 1-D grid of 8 * nt8 * NBG blocks (eelg_capi.hip): block b runs on XCD b % 8; the NBG group
+    # blocks of a tile are 8 apart (same XCD, dispatched together: gy rows and edge indices
+    # shared through one L2)
+    L.append(f"  const int bi = blockIdx.x >> 3, by = bi % {nbg};")
+    L.append(f"  const int n0 = ((bi / {nbg}) * 8 + (blockIdx.x & 7)) * {R};")
+    L.append("  if (n0 >= n_nodes) return;")
+    L.append(f"  const int sg = bwf_sg_{name}[by];")
+    # ---- stage 1: grad_agg of the group's slots for the tile (MFMA into LDS) ----
+    # the operands of task t + 4 are loaded while task t's MFMAs run (P1)
+    L.append(f"  const int t1 = bwf_tb_{name}[by + 1]{' * 0' if TP_BWF_SKIP == 2 else ''};")
+    L.append("  int t = bwf_tb_" + name + "[by] + wave;")
+
+    def p1_load(pre, tv):
+        return [f"  eelg_bwf_task {pre}tk = {tn}[{tv} < t1 ? {tv} : t1 - 1];",
+                f"  int {pre}col = {pre}tk.ct * 32 + u, {pre}r = {pre}col / {pre}tk.d3, {pre}m = {pre}col - {pre}r * {pre}tk.d3;",
+                f"  bool {pre}ok = {tv} < t1 && {pre}r < {R} && n0 + {pre}r < n_nodes;",
+                f"  eelg_f4a {pre}a0, {pre}a1, {pre}a2, {pre}a3; float {pre}b[16];",
+                f"  {{ const float* __restrict__ gp = gy + (size_t)(n0 + ({pre}ok ? {pre}r : 0)) * {tdim} + {pre}tk.gyoff + {pre}m + hf * 16 * {pre}tk.d3;",
+                f"    const eelg_f4a* __restrict__ wp = reinterpret_cast<const eelg_f4a*>(wl + {pre}tk.woff + u * 32 + hf * 16);",
+                f"    {pre}a0 = wp[0]; {pre}a1 = wp[1]; {pre}a2 = wp[2]; {pre}a3 = wp[3];",
+                "#pragma unroll",
+                f"    for (int st = 0; st < 16; ++st) {pre}b[st] = {pre}ok ? gp[st * {pre}tk.d3] : 0.0f; }}"]
+    if P1:
+        L.append("  if (t < t1) {")
+        L += ["  " + ln for ln in p1_load("", "t")]
+        L.append("  for (;;) {")
+        L += ["  " + ln for ln in p1_load("n", "t + 4")]
+    else:
+        L.append("  for (; t < t1; t += 4) {")
+        L += p1_load("", "t")
+    L.append("    eelg_f32x16v acc = {};")
+    for st in range(16):
+        L.append(f"    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a{st // 4}[{st % 4}], b[{st}], acc, 0, 0, 0);")
+    L.append("    if (ok) {")
+    L.append("      float* __restrict__ gd = Gs + r * sg + tk.lds + 4 * hf * tk.d3 + m;")
+    L.append("#pragma unroll")
+    L.append("      for (int v = 0; v < 16; ++v) gd[((v & 3) + 8 * (v >> 2)) * tk.d3] = acc[v] * tk.alpha;")
+    L.append("    }")
+    if P1:
+        L.append("    t += 4;")
+        L.append("    if (t >= t1) break;")
+        L.append("    tk = ntk; col = ncol; r = nr; m = nm; ok = nok; a0 = na0; a1 = na1; a2 = na2; a3 = na3;")
+        L.append("#pragma unroll")
+        L.append("    for (int st = 0; st < 16; ++st) b[st] = nb[st];")
+        L.append("  }}")
+    else:
+        L.append("  }")
+    L.append("  __syncthreads();")
+    # ---- stage 2: the tile's in-edges, tp_bwd's per-path arithmetic with grad_agg from LDS ----
+    L.append("  const int hw = threadIdx.x >> 5;")
+    if TP_BWF_SKIP == 1:
+        L.append("  if (n_nodes > 0) return;")
+    if EM:
+        # edge-major: half-wave hw takes edges eb + hw, eb + hw + 8, ... of the tile's range
+        L.append(f"  const int eb = rowptr[n0] + hw, ee = rowptr[min(n0 + {R}, n_nodes)];")
+        ES = 8
+    else:
+        # receiver-major: half-wave hw streams the in-edges of receiver n0 + hw
+        L.append(f"  if (hw >= {R} || n0 + hw >= n_nodes) return;")
+        L.append("  const int eb = rowptr[n0 + hw], ee = rowptr[n0 + hw + 1];")
+        ES = 1
+    L.append("  if (eb >= ee) return;")
+    L.append("  switch (by) {")
+    PF = TP_BWD_PFD
+    for gi, grp in enumerate(bgroups):
+        l = grp[0].l1
+        d = 2 * l + 1
+        sg = sgs[gi]
+        l2s = sorted({p.l2 for p in grp})
+        xs_ = [f"x{l}_{i}" for i in range(d)]
+        ys_ = [f"y{l2 * l2 + j}" for l2 in l2s for j in range(2 * l2 + 1)]
+        p0 = grp[0]
+        L.append(f"  case {gi}: {{ // input block l1 = {l}")
+        if not EM:
+            L.append(f"    const float* __restrict__ gr = Gs + hw * {sg};")
+
+        def edge_loads(pref, sv, ev):
+            out = [f"    {{ const float* __restrict__ xs = x + (size_t){sv} * {din};",
+                   f"      const float* __restrict__ ye = sh + (size_t){ev} * {nshp};",
+                   f"      const {WT}* __restrict__ we = w + (size_t){ev} * {wn} + u;"]
+            out += ["      " + ln for ln in vec_load([pref + v for v in xs_], "xs", f"{node_off[l]} + u * {d}")]
+            out += ["      " + ln for ln in sh_load(l2s, pref, "ye")]
+            out.append(f"      {pref}w{p0.slot} = {ld_w(f'we[{p0.slot * MUL}]')};")
+            out.append("    }")
+            return out
+        carried = xs_ + ys_ + [f"w{p0.slot}"]
+        if NX:
+            L.append("    float " + ", ".join(carried) + ";")
+            L += edge_loads("", "sender[eb]", "eb")
+        L.append(f"    for (int e = eb; e < ee; e += {ES}) {{")
+        if NX:
+            L.append(f"      const bool more = e + {ES} < ee;")
+            L.append(f"      const int sn = more ? sender[e + {ES}] : 0, en = more ? e + {ES} : e;")
+        else:
+            L.append("      float " + ", ".join(carried) + ";")
+            L += ["  " + ln for ln in edge_loads("", "sender[e]", "e")]
+        if EM:
+            L.append(f"      const float* __restrict__ gr = Gs + (receiver[e] - n0) * {sg};")
+        L.append(f"      const {WT}* __restrict__ we = w + (size_t)e * {wn} + u;")
+        L.append(f"      {WT}* __restrict__ gwe = gw + (size_t)e * {wn} + u;")
+        L.append(f"      {WT}* __restrict__ gxo = gxe + (size_t)e * {din};")
+        for i in range(d):
+            L.append(f"      float gx{l}_{i} = 0.0f;")
+        if NX:
+            L.append("      float " + ", ".join("n" + v for v in carried) + ";")
+        base_pin = xs_ + [f"gx{l}_{i}" for i in range(d)] + ys_
+        wregs = {0: [f"w{p0.slot}"]}
+        for pj in range(1, min(PF, len(grp))):
+            L.append(f"      float w{grp[pj].slot} = {ld_w(f'we[{grp[pj].slot * MUL}]')};")
+            wregs[pj] = [f"w{grp[pj].slot}"]
+        for pi, p in enumerate(grp):
+            d3 = 2 * p.l3 + 1
+            d1 = 2 * p.l1 + 1
+            if pi + PF < len(grp):
+                q = grp[pi + PF]
+                L.append(f"      float w{q.slot} = {ld_w(f'we[{q.slot * MUL}]')};")
+                wregs[pi + PF] = [f"w{q.slot}"]
+            if pi + 1 < len(grp):
+                nxt_regs = wregs[pi + 1]
+            elif NX:                         # next edge's loads in flight during the last path
+                L += ["  " + ln for ln in edge_loads("n", "sn", "en")]
+                nxt_regs = ["n" + v for v in carried]
+            else:
+                nxt_regs = []
+            L.append(f"      {{ // slot {p.slot}: {p.l1} x {p.l2} -> {p.l3}")
+            L.append(f"        const float* __restrict__ gs = gr + {lds_of[p.slot]} + u * {d3};")
+            L.append("        const float " + ", ".join(f"g{p.slot}_{k} = gs[{k}]" for k in range(d3)) + ";")
+            L.append(f"        const float cp = {flit(p.coef)} * inv_norm;")
+            byik: Dict[Tuple[int, int], List[str]] = {}
+            for (i, j, k), c in _path_cg(p):
+                byik.setdefault((i, k), []).append(f"{flit(c)} * y{p.l2 * p.l2 + j}")
+            for (i, k), ts in byik.items():
+                L.append(f"        const float m{i}_{k} = {' + '.join(ts)};")
+            gterms = []
+            for k in range(d3):
+                ts = [f"x{p.l1}_{i} * m{i}_{k}" for i in range(d1) if (i, k) in byik]
+                if ts:
+                    gterms.append(f"g{p.slot}_{k} * ({' + '.join(ts)})")
+            gexpr = " + ".join(gterms) if gterms else "0.0f"
+            if TP_BWD_NT and not bf:
+                L.append(f"        __builtin_nontemporal_store(cp * ({gexpr}), &gwe[{p.slot * MUL}]);")
+            else:
+                L.append(f"        gwe[{p.slot * MUL}] = {st_w(f'cp * ({gexpr})')};")
+            L.append(f"        const float hw_ = cp * w{p.slot};")
+            for i in range(d1):
+                ts = [f"m{i}_{k} * g{p.slot}_{k}" for k in range(d3) if (i, k) in byik]
+                if ts:
+                    L.append(f"        gx{p.l1}_{i} = fmaf(hw_, {' + '.join(ts)}, gx{p.l1}_{i});")
+            L.append("      }")
+            L.append("      " + pin(base_pin + nxt_regs))
+        if bf:
+            L += [f"      gxo[{node_off[l]} + u * {d} + {i}] = eelg_f2bf(gx{l}_{i});" for i in range(d)]
+        else:
+            L += ["      " + ln for ln in vec_store([f"gx{l}_{i}" for i in range(d)], "gxo", f"{node_off[l]} + u * {d}",
+                                                       nt=bool(TP_BWD_NT))]
+        if NX:
+            L.append("      " + " ".join(f"{v} = n{v};" for v in carried))
+        L.append("    }")
+        L.append("    break; }")
+    L.append("  default: break;")
+    L.append("  }")
+    L.append("}")
+    return L
+
+
 def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32") -> Tuple[str, dict]:
     """``wt`` = "f32" | "bf16": storage type of the edge-sized tensors (TP weights w and
     grad_w, per-edge grad gxe); arithmetic is fp32 either way (BASELINE config 5)."""
@@ -872,8 +1121,13 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     L.append("  default: break;")
     L.append("  }")
     L.append("}")
+    # fused output-linear grad-x + backward (mul 32: one channel group of 32 lanes)
+    bwf = CG == 1 and LW == 32
+    if bwf:
+        L += _emit_tp_bwf(name, sfx, bgroups, paths, target, din, nshp, wn, node_off, bf, ld_w, st_w)
     info = dict(din=din, dmid=dmid, wn=wn, nsh=nsh, ngroups=len(groups) * CG, nbgroups=len(bgroups) * CG,
                 npaths=len(paths), nph=TP_NPH, beph=TP_BWD_EPH, fwpb=TP_FWD_WPB, bxcd=TP_BWD_XCD,
+                bwf=int(bwf), bwf_r=TP_BWF_R, tdim=target.dim,
                 sig=fnv1a64(tp_signature(node, sh, target)))
     return "\n".join(L), info
 
@@ -2271,9 +2525,11 @@ def main(outdir: str) -> None:
             lmax = int(name.split("_l")[1].split("_")[0])
             bfk = (f"tp_fwd_{name}_bw, tp_bwd_{name}_bw, tp_bws_{name}, tp_bws_{name}_bw" if bf
                    else f"nullptr, nullptr, tp_bws_{name}, nullptr")
+            bwk = (f"tp_bwf_{name}, " + (f"tp_bwf_{name}_bw" if bf else "nullptr")) if i["bwf"] else "nullptr, nullptr"
+            bws_ = f"bwf_slots_{name}, bwf_alpha_{name}" if i["bwf"] else "nullptr, nullptr"
             parts.append(f'  {{"{name}", {i["din"]}, {i["dmid"]}, {i["wn"]}, {i["nsh"]}, {i["ngroups"]}, '
                          f'{i["npaths"]}, {lmax}, {i["nbgroups"]}, {i["nph"]}, {i["beph"]}, {i["fwpb"]}, 0x{i["sig"]:016x}ULL, tp_fwd_{name}, tp_bwd_{name}, '
-                         f'{bfk}, {i["ngroups_bf"]}, {i["bxcd"]}}},')
+                         f'{bfk}, {i["ngroups_bf"]}, {i["bxcd"]}, {bwk}, {i["bwf_r"]}, {i["tdim"]}, {bws_}}},')
         parts.append("};")
         parts.append("static const eelg_sc_cfg kScConfigs[] = {")
         for name, i in sc_table:

@@ -36,6 +36,9 @@ _SIGS = {
     "eelg_tp_bwd_sorted_bf16": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_tp_bwd_sender": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
     "eelg_tp_bwd_sender_bf16": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _F, _P, _P, _P], _I),
+    "eelg_tp_bwd_fused": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P], _I),
+    "eelg_tp_bwd_fused_bf16": ([_I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P], _I),
+    "eelg_tp_bwf_slot": ([_I, _I, _P, _P, _P], _I),
     "eelg_segment_sum_csr": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_csr_bf16": ([_P, _P, _P, _P, _F, _I, _I, _P, _P], _I),
     "eelg_segment_sum_split": ([_P, _P, _P, _P, _F, _I, _I, _I, _P, _P, _P], _I),

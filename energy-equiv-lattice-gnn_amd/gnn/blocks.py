@@ -270,6 +270,12 @@ class TensorProductInteractionBlock(torch.nn.Module):
             self._cfg = _lib.tp_config_by_sig(self._sig)
         return self._cfg
 
+    def _bwf(self, cfg: int) -> bool:
+        """the fused linear + TP backward serves this block (generated, same linear layout)"""
+        if not hasattr(self, "_tp_paths"):
+            self._tp_paths = cg.tp_paths(self._node_feats_irreps, self.edge_attrs_irreps, self._irreps_out)
+        return ops.tp_linear_fusable(cfg, self.linear, self._tp_paths)
+
     def radial_weights(self, edge_feats: torch.Tensor) -> torch.Tensor:
         """``conv_tp_weights(edge_feats)`` (``gnn/blocks.py:590``): the per-edge TP weights."""
         if self._radial_hip:
@@ -292,6 +298,9 @@ class TensorProductInteractionBlock(torch.nn.Module):
             w = self.radial_weights(edge_feats)
         inv = 1.0 / self.agg_norm_const
         if self.reduce in ("sum", "add"):
+            if ops.TP_BWF and self._bwf(idx):
+                # output linear + TP with one fused backward kernel (eelg_tp_bwd_fused)
+                return ops.tp_interaction_linear(x, edge_attrs, w, csr, idx, info, inv, self.linear), None
             agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv)
         elif self.reduce == "mean":
             agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv) * ops.in_degree_scale(csr)[:, None]

@@ -74,6 +74,12 @@ RADIAL_CHAIN = os.environ.get("EELG_RADIAL_CHAIN", "1") != "0"
 TP_BWD_SPOS = os.environ.get("EELG_TP_BWD_SPOS", "0") != "0"
 _TBS = os.environ.get("EELG_TP_BWD_SENDER", "0")
 TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
+# fused backward of the interaction's output linear and the TP (eelg_tp_bwd_fused): the
+# linear's grad-x [N, dmid] is computed per receiver tile into LDS inside the TP backward instead
+# of being written to HBM by the linear and read back by tp_bwd.  Measured slower (r09c kbench:
+# 1.10 ms vs 0.68 + 0.32 ms for tp_bwd + the linear's grad-x; r09a step 2002 vs ~2190 graphs/s):
+# the per-tile MFMA stage is latency-bound at the occupancy its LDS block allows.  Off by default.
+TP_BWF = os.environ.get("EELG_TP_BWF", "0") != "0"
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
@@ -320,31 +326,7 @@ class _TPInteraction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
         # w: fp32, or bf16 storage (BASELINE config 5; fp32 arithmetic in the kernels)
-        bf = w.dtype == torch.bfloat16
-        x = _a16(x)
-        if bf:
-            w = w.contiguous()
-            w = w if w.data_ptr() % 16 == 0 else w.clone()
-        else:
-            w = _a16(w)
-        if sh.dtype != torch.float32:
-            raise TypeError(f"expected float32 SH, got {sh.dtype}")
-        sh = padded_sh(sh)
-        n = x.shape[0]
-        if x.shape[1] != info["din"] or sh.shape[1] != info["nsh"] or w.shape[1] != info["wn"]:
-            raise ValueError(f"shape mismatch: x {tuple(x.shape)} sh {tuple(sh.shape)} "
-                             f"w {tuple(w.shape)} vs config {info}")
-        if sh.shape[0] != csr.num_edges or w.shape[0] != csr.num_edges or n != csr.num_nodes:
-            raise ValueError("edge/node counts do not match the CSR")
-        n_out = csr.rowptr.shape[0] - 1        # receivers (nodes; edges for per_edge_csr)
-        agg = torch.empty(n_out, info["dmid"], device=x.device, dtype=torch.float32)
-        lib = _lib.load()
-        tok = TIMER.start(f"tp_fwd[din={info['din']}]")
-        fwd = lib.eelg_tp_fwd_bf16 if bf else lib.eelg_tp_fwd
-        _lib.check(fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
-                       _lib.ptr(csr.rowptr), n_out, float(inv_norm), _lib.ptr(agg), _lib.stream(agg)),
-                   "tp_fwd")
-        TIMER.stop(tok)
+        agg, x, sh, w = _tp_fwd(x, sh, w, csr, cfg, info, inv_norm)
         ctx.save_for_backward(x, sh, w)
         ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm = csr, cfg, info, inv_norm
         return agg
@@ -385,6 +367,153 @@ class _TPInteraction(torch.autograd.Function):
 def tp_interaction(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
     _require_device(x, sh, w)
     return _TPInteraction.apply(x, sh, w, csr, cfg, info, inv_norm)
+
+
+def _tp_fwd(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: float):
+    """tp_fwd launch with the input checks of ``_TPInteraction``; returns (agg, x, sh, w) with
+    the operands as the kernels read them"""
+    bf = w.dtype == torch.bfloat16
+    x = _a16(x)
+    if bf:
+        w = w.contiguous()
+        w = w if w.data_ptr() % 16 == 0 else w.clone()
+    else:
+        w = _a16(w)
+    if sh.dtype != torch.float32:
+        raise TypeError(f"expected float32 SH, got {sh.dtype}")
+    sh = padded_sh(sh)
+    n = x.shape[0]
+    if x.shape[1] != info["din"] or sh.shape[1] != info["nsh"] or w.shape[1] != info["wn"]:
+        raise ValueError(f"shape mismatch: x {tuple(x.shape)} sh {tuple(sh.shape)} "
+                         f"w {tuple(w.shape)} vs config {info}")
+    if sh.shape[0] != csr.num_edges or w.shape[0] != csr.num_edges or n != csr.num_nodes:
+        raise ValueError("edge/node counts do not match the CSR")
+    n_out = csr.rowptr.shape[0] - 1
+    agg = torch.empty(n_out, info["dmid"], device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    tok = TIMER.start(f"tp_fwd[din={info['din']}]")
+    fwd = lib.eelg_tp_fwd_bf16 if bf else lib.eelg_tp_fwd
+    _lib.check(fwd(cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
+                   _lib.ptr(csr.rowptr), n_out, float(inv_norm), _lib.ptr(agg), _lib.stream(agg)),
+               "tp_fwd")
+    TIMER.stop(tok)
+    return agg, x, sh, w
+
+
+_BWF_OK: Dict[tuple, bool] = {}
+
+
+def tp_linear_fusable(cfg: int, lin, paths) -> bool:
+    """whether ``eelg_tp_bwd_fused`` serves ``lin(tp_interaction(...))`` for TP config ``cfg``:
+    generated for it (mul 32), and its slot table (weight offset, alpha, gy offset per TP slot)
+    equals what ``lin`` (an ``o3.Linear`` over the TP's output irreps) computes.  ``paths``:
+    ``cg.tp_paths`` of the block (slot, l3, out_off).  Cached per (cfg, linear)."""
+    key = (cfg, id(lin))
+    if key in _BWF_OK:
+        return _BWF_OK[key]
+    ok = _bwf_table_matches(cfg, lin, paths)
+    _BWF_OK[key] = ok
+    return ok
+
+
+def _bwf_table_matches(cfg: int, lin, paths) -> bool:
+    lib = _lib.load()
+    wo, al, go = ctypes.c_int(), ctypes.c_float(), ctypes.c_int()
+    if lin.bias_slots and any(lin.irreps_out[o].ir.l != 0 for o in lin.bias_slots):
+        return False
+    ins_of_in = {}
+    for t, (i, o) in enumerate(lin.instructions):
+        if i in ins_of_in:                 # an input block read by two outputs: not the TP layout
+            return False
+        ins_of_in[i] = (t, o)
+    for p in paths:
+        if lib.eelg_tp_bwf_slot(cfg, p.slot, ctypes.byref(wo), ctypes.byref(al), ctypes.byref(go)) != 0:
+            return False
+        hit = None
+        for i, (mul, ir) in enumerate(lin.irreps_in):
+            lo = lin._in_off[i]
+            if lo <= p.out_off < lo + mul * ir.dim and ir.l == p.l3:
+                hit = i
+                break
+        if hit is None or hit not in ins_of_in:
+            return False
+        t, o = ins_of_in[hit]
+        d = 2 * p.l3 + 1
+        q, rem = divmod(p.out_off - lin._in_off[hit], 32 * d)
+        mo = lin.irreps_out[o].mul
+        if rem or mo != 32 or p.mul != 32:
+            return False
+        if (wo.value != lin._w_offs[t] + q * 32 * mo or go.value != lin._out_off[o]
+                or abs(al.value - lin.alpha[t]) > 1e-6 * lin.alpha[t]):
+            return False
+    return True
+
+
+class _TPInteractionLinear(torch.autograd.Function):
+    """``lin(tp_interaction(x, sh, w))``: the forward runs tp_fwd and the linear as two kernels;
+    the backward runs the linear's weight / bias gradients (side stream) and ONE fused kernel
+    for the TP's grad-x / grad-w from the linear's output gradient (``eelg_tp_bwd_fused``)."""
+
+    @staticmethod
+    def forward(ctx, x, sh, w, lw, lb, csr: EdgeCSR, cfg: int, info: Dict[str, int],
+                inv_norm: float, lin, side):
+        agg, x, sh, w = _tp_fwd(x, sh, w, csr, cfg, info, inv_norm)
+        y = lin._fwd(agg, lw, lb)
+        ctx.save_for_backward(x, sh, w, agg, lw)
+        ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm, ctx.lin, ctx.side = csr, cfg, info, inv_norm, lin, side
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, sh, w, agg, lw = ctx.saved_tensors
+        csr, info, lin, side = ctx.csr, ctx.info, ctx.lin, ctx.side
+        gy = _a16(gy)
+        want_w, want_b = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        gW = gb = None
+        if want_w or want_b:
+            if side is None:
+                gW = lin._bwd_w(agg, gy) if want_w else None
+                gb = lin._bwd_bias(gy) if want_b else None
+            else:
+                side.wait_stream(torch.cuda.current_stream(gy.device))
+                agg.record_stream(side)
+                gy.record_stream(side)
+                with torch.cuda.stream(side):
+                    gW = lin._bwd_w(agg, gy) if want_w else None
+                    gb = lin._bwd_bias(gy) if want_b else None
+        lwc = lw.detach().contiguous()
+        if lwc.data_ptr() % 16:
+            lwc = lwc.clone()
+        gw = torch.empty_like(w)
+        gxe = torch.empty(csr.num_edges, info["din"], device=x.device, dtype=w.dtype)
+        lib = _lib.load()
+        bwf = lib.eelg_tp_bwd_fused_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_fused
+        tok = TIMER.start(f"tp_bwf[din={info['din']}]")
+        _lib.check(bwf(ctx.cfg, _lib.ptr(x), _lib.ptr(sh), _lib.ptr(w), _lib.ptr(csr.sender),
+                       _lib.ptr(csr.receiver), _lib.ptr(csr.rowptr), csr.num_nodes, _lib.ptr(gy), _lib.ptr(lwc),
+                       float(ctx.inv_norm), _lib.ptr(gw), _lib.ptr(gxe), _lib.stream(gxe)),
+                   "tp_bwd_fused")
+        TIMER.stop(tok)
+        gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
+        return gx, None, gw, gW, gb, None, None, None, None, None, None
+
+
+def tp_interaction_linear(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int],
+                          inv_norm: float, lin):
+    """``lin(tp_interaction(x, sh, w, csr, cfg, info, inv_norm))`` with the fused backward;
+    the caller checks ``tp_linear_fusable`` first.  ``lin``'s weight / bias gradients run on
+    its side stream as ``o3.Linear.forward`` arranges them."""
+    _require_device(x, sh, w)
+    from .o3 import _OnStream
+    lw, lb = lin.weight, lin.bias
+    side = None
+    if OVERLAP and x.is_cuda and torch.is_grad_enabled() and lw.requires_grad:
+        side = side_stream(x.device, 2)
+        with torch.cuda.stream(side):
+            lw = _OnStream.apply(lw, side)
+            if lb is not None:
+                lb = _OnStream.apply(lb, side)
+    return _TPInteractionLinear.apply(x, sh, w, lw, lb, csr, cfg, info, inv_norm, lin, side)
 
 
 def per_edge_csr(csr: EdgeCSR) -> EdgeCSR:

@@ -105,6 +105,27 @@ int eelg_tp_bwd_sender_bf16(int cfg, const float* x, const float* sh, const void
                             int n_nodes, const float* grad_agg, float inv_norm, void* grad_w,
                             float* grad_x, void* stream);
 
+/* Fused backward of linear(tp_interaction(x, sh, w)) -- the interaction's output o3.Linear
+ * (7360 -> 800 at lmax 4) and the fused TP + scatter -- w.r.t. x and w, from the linear's output
+ * gradient gy [n_nodes, target dim] and its flat weight lin_w (16-B aligned).  Replaces the
+ * linear's grad-x followed by eelg_tp_bwd (gnn/blocks.py:591-604 autograd): grad_agg is computed
+ * per receiver tile into LDS and never written to HBM.  Writes grad_w [E, wn] and the per-edge
+ * grad_x rows gxe [E, din] in receiver-sorted edge order, as eelg_tp_bwd; rowptr is the receiver
+ * CSR (int32 [n_nodes + 1]) and receiver the sorted edges' receivers (int32 [E]).  Generated for mul 32; returns -2 for other configs.  The linear
+ * is o3.Linear(irreps_mid.simplify(), target): eelg_tp_bwf_slot returns, per TP slot, the
+ * weight offset of its 32 x 32 block, its alpha and its gy offset, for the caller to check
+ * against its own linear before using this path. */
+int eelg_tp_bwd_fused(int cfg, const float* x, const float* sh, const float* w, const int* sender,
+                      const int* receiver,
+                      const int* rowptr, int n_nodes, const float* gy, const float* lin_w,
+                      float inv_norm, float* grad_w, float* gxe, void* stream);
+int eelg_tp_bwd_fused_bf16(int cfg, const float* x, const float* sh, const void* w,
+                           const int* sender, const int* receiver, const int* rowptr,
+                           int n_nodes, const float* gy,
+                           const float* lin_w, float inv_norm, void* grad_w, void* gxe,
+                           void* stream);
+int eelg_tp_bwf_slot(int cfg, int slot, int* w_off, float* alpha, int* gy_off);
+
 /* CSR segmented sum (deterministic, no atomics):
  * out[r, :] = scale * row_scale[r] * sum_{j in [rowptr[r], rowptr[r+1])} src[idx ? idx[j] : j, :].
  * Replaces torch_scatter.scatter(..., reduce='sum'|'mean') (gnn/blocks.py:595-597,

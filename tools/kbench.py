@@ -129,6 +129,19 @@ def main():
                                        ops._lib.stream(x)), "tp_bwd")
     bwd_bytes = 4 * (n * 800 + e * 25 + 2 * e * info["wn"] + 2 * e + e * 800 + n * info["dmid"])
     rec("tp_bwd (B)", timeit_if("tp_bwd (B)", tpb, args.reps), bwd_bytes, 2 * tp_flops)
+    # fused output-linear grad-x + TP backward (replaces lin 7360->800 bwd_x + tp_bwd)
+    gyl = torch.randn(n, 800, device=dev)
+    lw = blk.linear.weight.detach().contiguous()
+
+    def tpbf():
+        ops._lib.check(lib.eelg_tp_bwd_fused(idx, ops._lib.ptr(x), ops._lib.ptr(sh), ops._lib.ptr(w),
+                                             ops._lib.ptr(csr.sender), ops._lib.ptr(csr.receiver),
+                                             ops._lib.ptr(csr.rowptr), n,
+                                             ops._lib.ptr(gyl), ops._lib.ptr(lw), 0.25, ops._lib.ptr(gw),
+                                             ops._lib.ptr(gxe), ops._lib.stream(x)), "tp_bwf")
+    bwf_bytes = 4 * (n * 800 + e * 25 + 2 * e * info["wn"] + 2 * e + e * 800 + n * 800 + n + 1)
+    rec("tp_bwf (B, fused linear)", timeit_if("tp_bwf (B, fused linear)", tpbf, args.reps), bwf_bytes,
+        2 * tp_flops + 2 * n * 7360 * 32)
     rec("segment_sum gxe->gx (800)", timeit_if("segment_sum gxe->gx (800)", lambda: ops.segment_sum_csr(gxe, csr.srowptr, n, idx=csr.sperm), args.reps),
         4 * (e * 800 + n * 800 + 2 * e))
     m7360 = torch.randn(e, 7360, device=dev)
