@@ -301,6 +301,10 @@ class TensorProductInteractionBlock(torch.nn.Module):
             if ops.TP_BWF and self._bwf(idx):
                 # output linear + TP with one fused backward kernel (eelg_tp_bwd_fused)
                 return ops.tp_interaction_linear(x, edge_attrs, w, csr, idx, info, inv, self.linear), None
+            if ops.TP_BWC > 1 and x.requires_grad:
+                # the linear's grad-x and tp_bwd interleaved per receiver chunk
+                return ops.tp_interaction_linear(x, edge_attrs, w, csr, idx, info, inv, self.linear,
+                                                 ops.TP_BWC), None
             agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv)
         elif self.reduce == "mean":
             agg = ops.tp_interaction(x, edge_attrs, w, csr, idx, info, inv) * ops.in_degree_scale(csr)[:, None]

@@ -80,11 +80,18 @@ TP_BWD_SENDER = None if _TBS == "auto" else _TBS != "0"
 # 1.10 ms vs 0.68 + 0.32 ms for tp_bwd + the linear's grad-x; r09a step 2002 vs ~2190 graphs/s):
 # the per-tile MFMA stage is latency-bound at the occupancy its LDS block allows.  Off by default.
 TP_BWF = os.environ.get("EELG_TP_BWF", "0") != "0"
+# the output linear's grad-x and tp_bwd in C node chunks (C > 1): each chunk's grad_agg rows
+# (N / C x 29 KB) are read back by tp_bwd right after the linear wrote them, from the 256 MB
+# MALL instead of HBM (chunk edge ranges from one host read of the CSR, cached per graph).
+# Bitwise equal to the one-pass kernels; measured slower (r09g, same box, default 2205 / 2200
+# graphs/s: C 4 2171, C 8 2121, C 16 2007) -- each extra launch pair adds two kernel tails.
+TP_BWC = int(os.environ.get("EELG_TP_BWC", "0"))
 _SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
 
 
 def side_stream(device, which: int = 0) -> "torch.cuda.Stream":
-    """Side stream ``which`` of ``device``: 0 = radial MLPs, 1 = contraction coefficients."""
+    """Side stream ``which`` of ``device``: 0 = radial MLPs, 1 = contraction coefficients,
+    2 = linear weight gradients."""
     idx = torch.device(device).index
     idx = torch.cuda.current_device() if idx is None else idx
     if (idx, which) not in _SIDE:
@@ -456,11 +463,12 @@ class _TPInteractionLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, sh, w, lw, lb, csr: EdgeCSR, cfg: int, info: Dict[str, int],
-                inv_norm: float, lin, side):
+                inv_norm: float, lin, side, chunks: int = 0):
         agg, x, sh, w = _tp_fwd(x, sh, w, csr, cfg, info, inv_norm)
         y = lin._fwd(agg, lw, lb)
         ctx.save_for_backward(x, sh, w, agg, lw)
         ctx.csr, ctx.cfg, ctx.info, ctx.inv_norm, ctx.lin, ctx.side = csr, cfg, info, inv_norm, lin, side
+        ctx.chunks = chunks
         return y
 
     @staticmethod
@@ -481,10 +489,12 @@ class _TPInteractionLinear(torch.autograd.Function):
                 with torch.cuda.stream(side):
                     gW = lin._bwd_w(agg, gy) if want_w else None
                     gb = lin._bwd_bias(gy) if want_b else None
+        gw = torch.empty_like(w)
+        if ctx.chunks > 1:
+            return _tp_linear_bwd_chunked(ctx, x, sh, w, lw, gy, gw) + (gW, gb) + (None,) * 7
         lwc = lw.detach().contiguous()
         if lwc.data_ptr() % 16:
             lwc = lwc.clone()
-        gw = torch.empty_like(w)
         gxe = torch.empty(csr.num_edges, info["din"], device=x.device, dtype=w.dtype)
         lib = _lib.load()
         bwf = lib.eelg_tp_bwd_fused_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_fused
@@ -495,11 +505,57 @@ class _TPInteractionLinear(torch.autograd.Function):
                    "tp_bwd_fused")
         TIMER.stop(tok)
         gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
-        return gx, None, gw, gW, gb, None, None, None, None, None, None
+        return gx, None, gw, gW, gb, None, None, None, None, None, None, None
+
+
+def _chunk_bounds(csr: EdgeCSR, chunks: int):
+    """[(n0, n1, e0, e1)]: ``chunks`` receiver ranges of about equal edge counts (one host read
+    of rowptr, cached on the CSR)"""
+    key = ("_chunks", chunks)
+    hit = getattr(csr, "_chunk_cache", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    rp = csr.rowptr.cpu()
+    n, e = csr.num_nodes, csr.num_edges
+    bounds, n0 = [], 0
+    for c in range(1, chunks + 1):
+        n1 = n if c == chunks else int(torch.searchsorted(rp, torch.tensor(e * c // chunks, dtype=rp.dtype)))
+        n1 = max(n0, min(n, n1))
+        if n1 > n0:
+            bounds.append((n0, n1, int(rp[n0]), int(rp[n1])))
+        n0 = n1
+    csr._chunk_cache = (key, bounds)
+    return bounds
+
+
+def _tp_linear_bwd_chunked(ctx, x, sh, w, lw, gy, gw):
+    """the unfused kernels (linear grad-x, tp_bwd) per receiver chunk: grad_agg of a chunk is
+    consumed while it is still in the MALL; tp_bwd's receiver indices are global, so its grad_agg
+    pointer is offset back by the chunk's first row"""
+    csr, info, lin = ctx.csr, ctx.info, ctx.lin
+    lib = _lib.load()
+    dmid, din, wn = info["dmid"], info["din"], info["wn"]
+    gxe = torch.empty(csr.num_edges, din, device=x.device, dtype=w.dtype)
+    esz = w.element_size()
+    bwd = lib.eelg_tp_bwd_sorted_bf16 if w.dtype == torch.bfloat16 else lib.eelg_tp_bwd_sorted
+    for n0, n1, e0, e1 in _chunk_bounds(csr, ctx.chunks):
+        gagg = lin._bwd_x(gy[n0:n1], lw)
+        if e1 <= e0:
+            continue
+        tok = TIMER.start(f"tp_bwd[din={din}]")
+        _lib.check(bwd(ctx.cfg, _lib.ptr(x), sh.data_ptr() + 4 * e0 * sh.stride(0),
+                       w.data_ptr() + esz * e0 * wn, csr.sender.data_ptr() + 4 * e0,
+                       csr.receiver.data_ptr() + 4 * e0, None, e1 - e0,
+                       gagg.data_ptr() - 4 * n0 * dmid, float(ctx.inv_norm),
+                       gw.data_ptr() + esz * e0 * wn, gxe.data_ptr() + esz * e0 * din,
+                       _lib.stream(gxe)), "tp_bwd")
+        TIMER.stop(tok)
+    gx = segment_sum_csr(gxe, csr.srowptr, csr.num_nodes, idx=csr.sperm)
+    return gx, None, gw
 
 
 def tp_interaction_linear(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int],
-                          inv_norm: float, lin):
+                          inv_norm: float, lin, chunks: int = 0):
     """``lin(tp_interaction(x, sh, w, csr, cfg, info, inv_norm))`` with the fused backward;
     the caller checks ``tp_linear_fusable`` first.  ``lin``'s weight / bias gradients run on
     its side stream as ``o3.Linear.forward`` arranges them."""
@@ -513,7 +569,7 @@ def tp_interaction_linear(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int]
             lw = _OnStream.apply(lw, side)
             if lb is not None:
                 lb = _OnStream.apply(lb, side)
-    return _TPInteractionLinear.apply(x, sh, w, lw, lb, csr, cfg, info, inv_norm, lin, side)
+    return _TPInteractionLinear.apply(x, sh, w, lw, lb, csr, cfg, info, inv_norm, lin, side, chunks)
 
 
 def per_edge_csr(csr: EdgeCSR) -> EdgeCSR:

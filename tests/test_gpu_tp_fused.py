@@ -95,3 +95,39 @@ def test_fused_table_rejects_other_linears():
     blk._bwf(idx)
     other = Linear(blk.irreps_mid, "64x0e+32x1o+32x2e+32x3o+32x4e")
     assert not ops.tp_linear_fusable(idx, other, blk._tp_paths)
+
+
+def _run_chunked(block, x, sh, ef, ei, go, chunks):
+    from gnn import ops
+    old = ops.TP_BWC
+    ops.TP_BWC = chunks
+    try:
+        return _run(block, x, sh, ef, ei, go, False)
+    finally:
+        ops.TP_BWC = old
+
+
+@pytest.mark.parametrize("lmax,n,e,isolated,chunks,storage", [
+    (4, 3000, 12000, 17, 8, "float32"),
+    (4, 50, 200, 3, 3, "float32"),
+    (4, 5, 9, 0, 8, "float32"),          # more chunks than receivers
+    (3, 777, 3100, 9, 4, "bfloat16"),
+])
+def test_chunked_linear_tp_backward_is_bitwise_unfused(lmax, n, e, isolated, chunks, storage):
+    """EELG_TP_BWC: the linear's grad-x and tp_bwd per receiver chunk run the same kernels on
+    row / edge sub-ranges, so every gradient equals the one-pass result bit for bit"""
+    from gnn.model import EnergyEquivGNN
+    torch.manual_seed(0)
+    m = EnergyEquivGNN(params(2, lmax=lmax, storage_dtype=storage)).to(DEV)
+    blk = m.stiffness_head.layers[1].interaction
+    ei = _graph(n, e, 11 + n, isolated).to(DEV)
+    x = torch.randn(n, blk.irreps_in.dim, device=DEV)
+    sh = torch.randn(e, (lmax + 1) ** 2, device=DEV)
+    ef = torch.rand(e, 12, device=DEV)
+    go = torch.randn(n, blk.irreps_out.dim, device=DEV)
+    y_ref, gx_ref, gp_ref = _run(blk, x, sh, ef, ei, go, False)
+    y, gx, gp = _run_chunked(blk, x, sh, ef, ei, go, chunks)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(gx, gx_ref)
+    for k in gp_ref:
+        assert torch.equal(gp[k], gp_ref[k]), k
