@@ -79,6 +79,9 @@ TP_BWD_NT = int(os.environ.get("EELG_TP_BWD_NT", "1"))
 # With 0 a receiver whose in-edges straddle two blocks has its grad_agg row fetched into two
 # L2s, and every XCD gathers every lattice's x rows
 TP_BWD_XCD = int(os.environ.get("EELG_TP_BWD_XCD", "2"))
+# tp_bwd: amdgpu_waves_per_eu floor (0: the compiler's 125 VGPRs, 4 waves / SIMD).  Round 6: 5
+# spills 87 VGPRs of tpB_l4 to scratch, 6 spills 303 -- the l4 kernel has no occupancy lever
+TP_BWD_WPE = int(os.environ.get("EELG_TP_BWD_WPE", "0"))
 # fused output-linear grad-x + TP backward (tp_bwf, mul 32; off by default, gnn/ops.py TP_BWF):
 # receivers per workgroup whose [Σ d3 × 32] grad_agg block of one input-block group is computed
 # by MFMA into LDS from the linear's output gradient, then read by the tile's in-edges.
@@ -900,7 +903,8 @@ def emit_tp(name: str, node: Irreps, sh: Irreps, target: Irreps, wt: str = "f32"
     bgroups = [[p for p in paths if p.l1 == l] for l in node_ls]
     bgroups = [g for g in bgroups if g]
     NBG = len(bgroups) * CG
-    L.append(f"__global__ __launch_bounds__(256) void tp_bwd_{name}{sfx}(")
+    bwpe = f" __attribute__((amdgpu_waves_per_eu({TP_BWD_WPE})))" if TP_BWD_WPE else ""
+    L.append(f"__global__ __launch_bounds__(256){bwpe} void tp_bwd_{name}{sfx}(")
     L.append(f"    const float* __restrict__ x, const float* __restrict__ sh, const {WT}* __restrict__ w,")
     L.append("    const int* __restrict__ sender, const int* __restrict__ receiver, int n_edges,")
     L.append("    const float* __restrict__ gagg, float inv_norm,")
