@@ -996,7 +996,9 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
     if (sl.bias_off >= 0 && sl.d != 1) return fail(-2, "linear_fwd: bias on a non-scalar slot");
   }
   if (n_nodes <= 0) return 0;
-  if (lin_fwd_fast_ok(x, x_row, y, y_row, desc) && !(res && (reinterpret_cast<uintptr_t>(res) & 15))) {
+  const bool full = lin_fwd_fast_ok(x, x_row, y, y_row, desc);
+  const bool part = !full && !res && LINF_PARTIAL && lin_fwd_fast_ok(x, x_row, y, y_row, desc, true);
+  if ((full || part) && !(res && (reinterpret_cast<uintptr_t>(res) & 15))) {
     // groups of 32/d whole nodes; the d = 9 slots have the most (ceil(n / 3))
     int max_groups = 0;
     for (int s = 0; s < desc->n_slots; ++s) {
@@ -1013,18 +1015,23 @@ int eelg_linear_fwd_res(const float* x, int x_row, const float* w, const float* 
     if (desc->max_jt == 1 && lds < LINF_LDS_1JT) lds = LINF_LDS_1JT;
     static bool lds_attr = false;   // > 64 KB of dynamic LDS must be allowed explicitly
     if (!lds_attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<false>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<false, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-          hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<true>),
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<true, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&lin_fwd_fast_kernel<false, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         return fail(-3, "linear_fwd: cannot raise the dynamic LDS limit");
       lds_attr = true;
     }
-    if (res)
-      hipLaunchKernelGGL(lin_fwd_fast_kernel<true>, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
+    if (part)
+      hipLaunchKernelGGL((lin_fwd_fast_kernel<false, true>), grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
+                         x, x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
+    else if (res)
+      hipLaunchKernelGGL((lin_fwd_fast_kernel<true, false>), grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
                          x, x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
     else
-      hipLaunchKernelGGL(lin_fwd_fast_kernel<false>, grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
+      hipLaunchKernelGGL((lin_fwd_fast_kernel<false, false>), grid, dim3(64 * LINF_WAVES), lds, (hipStream_t)stream,
                          x, x_row, w, bias, n_nodes, y, y_row, *desc, res, ws4);
     return check_launch("linear_fwd");
   }

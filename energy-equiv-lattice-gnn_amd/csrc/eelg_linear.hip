@@ -509,6 +509,11 @@ static bool lin_bwdw_fast_ok(const float* x, int x_row, const float* g, int g_ro
 #define LINF_PFD 1             // K chunks in flight per wave (1 or 2; 2 measured no faster)
 #endif
 #define LINF_KMAX 320          // sum of the slot's source K held in LDS
+// the fast kernel also takes partial column tiles / a partial single-source K chunk (the readout
+// tail's 32 -> 16-channel linear and its grad-x; they ran on lin_fwd_kernel at ~70 us each)
+#ifndef LINF_PARTIAL
+#define LINF_PARTIAL 1
+#endif
 #define LINF_XW 1152           // per-wave X region (floats) >= NB * SX for every D
 
 template <int D>
@@ -520,17 +525,19 @@ struct LinfGeom {
 };
 
 // ws[k][j] = alpha * W[k][jt*32 + j] for one source: BATCH loads per thread issued before their
-// LDS stores (clamped indices, guarded stores)
+// LDS stores (clamped indices, guarded stores).  Rows k in [src.k, 32 ceil(src.k / 32)) and
+// columns jt*32 + j >= n_out are zero (a partial K chunk / column tile)
 template <int BATCH>
 __device__ __forceinline__ void lin_stage_w(const float* __restrict__ w, const eelg_lin_src& src,
-                                            int jt, float* __restrict__ ws) {
-  const int tot = src.k * 32;
+                                            int jt, int n_out, float* __restrict__ ws) {
+  const int tot = (src.k + 31) / 32 * 32 * 32;
   for (int e0 = threadIdx.x; e0 < tot; e0 += BATCH * 64 * LINF_WAVES) {
     float v[BATCH];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       const int e = min(e0 + u * 64 * LINF_WAVES, tot - 1), k = e >> 5, jj = e & 31;
-      v[u] = w[src.w_off + (size_t)k * src.ldk + (size_t)(jt * 32 + jj) * src.ldj];
+      v[u] = (k < src.k && jt * 32 + jj < n_out)
+                 ? w[src.w_off + (size_t)k * src.ldk + (size_t)(jt * 32 + jj) * src.ldj] : 0.0f;
     }
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
@@ -552,7 +559,7 @@ typedef float linf_f4n __attribute__((ext_vector_type(4)));
 #else
 #define LINF_STORE(v, p) (*(p) = (v))
 #endif
-template <int D, bool RES>
+template <int D, bool RES, bool PART>
 __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_row,
                                              const float* __restrict__ bias, int n_nodes,
                                              float* __restrict__ y, int y_row,
@@ -563,7 +570,10 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   using G = LinfGeom<D>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hf = lane >> 5;
   int nch = 0;
-  for (int s = 0; s < sl.n_src; ++s) nch += sl.src[s].k / 32;
+  for (int s = 0; s < sl.n_src; ++s) nch += (sl.src[s].k + 31) / 32;
+  // PART: a partial last column tile (n_out % 32 != 0, a multiple of 4) -- float4 per node
+  // stored -- and partial K chunks; the full-tile instantiation keeps its register count
+  const int jw4 = PART ? min(32, sl.n_out - jt * 32) * D / 4 : G::RUN4;
   const int my_groups = g_base + wave < g_lim ? (g_lim - g_base - wave + LINF_WAVES - 1) / LINF_WAVES : 0;
   const int nq = my_groups * nch;
   if (nq == 0) return;
@@ -571,26 +581,29 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   const bool row_ok = i < G::NB * D;
   const int abase = (i / D) * G::SX + (i % D) + hf * D;
   const int bbase = hf * 32 + i;
-  const float bj = (sl.bias_off >= 0 && D == 1) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
-  auto chunk_of = [&](int q, int& group, int& xoff, int& kb) {
+  const float bj = (sl.bias_off >= 0 && D == 1 && (!PART || jt * 32 + i < sl.n_out)) ? bias[sl.bias_off + jt * 32 + i] : 0.0f;
+  // chunk q: node group, x offset, first weight row, and float4 per node run that hold data (a
+  // partial last K chunk, k % 32 != 0, reads only its k channels: the rest are zero)
+  auto chunk_of = [&](int q, int& group, int& xoff, int& kb, int& kv4) {
     const int k = q / nch;
     int c = q - k * nch;
     group = g_base + k * LINF_WAVES + wave;
     int s = 0;
     kb = 0;
-    while (c >= sl.src[s].k / 32) { c -= sl.src[s].k / 32; kb += sl.src[s].k; ++s; }
+    while (c >= (sl.src[s].k + 31) / 32) { c -= (sl.src[s].k + 31) / 32; kb += (sl.src[s].k + 31) / 32 * 32; ++s; }
     xoff = sl.src[s].x_off + c * 32 * D;
     kb += c * 32;
+    kv4 = PART ? min(32, sl.src[s].k - c * 32) * D / 4 : G::RUN4;
   };
   auto load = [&](int q, float4* r) {
-    int group, xoff, kb;
-    chunk_of(q, group, xoff, kb);
+    int group, xoff, kb, kv4;
+    chunk_of(q, group, xoff, kb, kv4);
     const int n0 = group * G::NB;
 #pragma unroll
     for (int qq = 0; qq < G::NQ; ++qq) {
       const int f = lane + 64 * qq;
       const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-      const bool ok = f < G::NB * G::RUN4 && n0 + a < n_nodes;
+      const bool ok = f < G::NB * G::RUN4 && n0 + a < n_nodes && w4 < kv4;
       r[qq] = ok ? *reinterpret_cast<const float4*>(x + (size_t)(n0 + a) * x_row + xoff + 4 * w4)
                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -600,8 +613,8 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   for (int t = 0; t < 16; ++t) acc[t] = bj;
   // one pipeline step: chunk q (registers r) to LDS, chunk q + LINF_PFD's loads into r, MFMAs
   auto step = [&](int q, float4* r) {
-    int group, xoff, kb;
-    chunk_of(q, group, xoff, kb);
+    int group, xoff, kb, kv4;
+    chunk_of(q, group, xoff, kb, kv4);
 #pragma unroll
     for (int qq = 0; qq < G::NQ; ++qq) {
       const int f = lane + 64 * qq;
@@ -641,7 +654,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
 #pragma unroll
         for (int qq = 0; qq < G::NQ; ++qq) {
           const int f = min(lane + 64 * qq, G::NB * G::RUN4 - 1);
-          const int a = f / G::RUN4, w4 = f - a * G::RUN4;
+          const int a = f / G::RUN4, w4 = PART ? min(f - a * G::RUN4, jw4 - 1) : f - a * G::RUN4;
           rr[qq] = *reinterpret_cast<const float4*>(rb + (size_t)min(n0 + a, n_nodes - 1) * y_row + 4 * w4);
         }
       }
@@ -649,7 +662,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
       for (int qq = 0; qq < G::NQ; ++qq) {
         const int f = lane + 64 * qq;
         const int a = f / G::RUN4, w4 = f - a * G::RUN4;
-        if (f < G::NB * G::RUN4 && n0 + a < n_nodes) {
+        if (f < G::NB * G::RUN4 && n0 + a < n_nodes && w4 < jw4) {
           const size_t o = (size_t)(n0 + a) * y_row + 4 * w4;
           float4 v = *reinterpret_cast<const float4*>(xw + a * G::SX + 4 * w4);
           if (RES) { v.x += rr[qq].x; v.y += rr[qq].y; v.z += rr[qq].z; v.w += rr[qq].w; }
@@ -673,7 +686,7 @@ __device__ __forceinline__ void lin_fwd_fast(const float* __restrict__ x, int x_
   }
 }
 
-template <bool RES>
+template <bool RES, bool PART>
 __device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ x, int x_row,
                                                const float* __restrict__ bias, int n_nodes,
                                                float* __restrict__ y, int y_row,
@@ -681,17 +694,17 @@ __device__ __forceinline__ void lin_fwd_fast_d(int d, const float* __restrict__ 
                                                const float* __restrict__ ws, float* __restrict__ xw,
                                                const float* __restrict__ res) {
   switch (d) {
-    case 1: lin_fwd_fast<1, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 3: lin_fwd_fast<3, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 5: lin_fwd_fast<5, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    case 7: lin_fwd_fast<7, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
-    default: lin_fwd_fast<9, RES>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 1: lin_fwd_fast<1, RES, PART>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 3: lin_fwd_fast<3, RES, PART>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 5: lin_fwd_fast<5, RES, PART>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    case 7: lin_fwd_fast<7, RES, PART>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
+    default: lin_fwd_fast<9, RES, PART>(x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res); break;
   }
 }
 
 // RES: the residual epilogue (y = x W + res), a separate instantiation so the plain linears
 // carry no residual registers
-template <bool RES>
+template <bool RES, bool PART>
 __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
     const float* __restrict__ x, int x_row, const float* __restrict__ w,
     const float* __restrict__ bias, int n_nodes, float* __restrict__ y, int y_row,
@@ -720,14 +733,14 @@ __global__ __launch_bounds__(64 * LINF_WAVES) void lin_fwd_fast_kernel(
   int kb = 0;
   for (int s = 0; s < sl.n_src; ++s) {
     const eelg_lin_src& src = sl.src[s];
-    if (src.k == 32) lin_stage_w<2>(w, src, jt, ws + kb * 32);
-    else lin_stage_w<8>(w, src, jt, ws + kb * 32);
-    kb += src.k;
+    if (src.k <= 32) lin_stage_w<2>(w, src, jt, sl.n_out, ws + kb * 32);
+    else lin_stage_w<8>(w, src, jt, sl.n_out, ws + kb * 32);
+    kb += (src.k + 31) / 32 * 32;
   }
   __syncthreads();
   float* xw = reinterpret_cast<float*>(xw4) + (threadIdx.x >> 6) * LINF_XW;
   const int g0 = gb * LINF_WAVES * LINF_GPW, g1 = min(n_groups, g0 + LINF_WAVES * LINF_GPW);
-  lin_fwd_fast_d<RES>(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
+  lin_fwd_fast_d<RES, PART>(d, x, x_row, bias, n_nodes, y, y_row, sl, g0, g1, jt, ws, xw, res);
 }
 
 // one column tile per slot (the 800 -> 800 linears): an LDS floor of 64 KB (two workgroups per
@@ -739,26 +752,30 @@ static void lin_fwd_fast_lds(const eelg_lin_desc* desc, int* ws4, size_t* bytes)
   int kmax = 0;
   for (int s = 0; s < desc->n_slots; ++s) {
     int kt = 0;
-    for (int t = 0; t < desc->slot[s].n_src; ++t) kt += desc->slot[s].src[t].k;
+    for (int t = 0; t < desc->slot[s].n_src; ++t) kt += (desc->slot[s].src[t].k + 31) / 32 * 32;
     kmax = kt > kmax ? kt : kmax;
   }
   *ws4 = kmax * 32 / 4;
   *bytes = (size_t)(*ws4) * 16 + (size_t)LINF_WAVES * LINF_XW * 4;
 }
 
+// partial: also slots whose n_out is a multiple of 4 but not of 32 (a partial last column tile)
+// and single-source slots whose K is a multiple of 4 but not of 32 (a partial last K chunk) --
+// the fp32 fast kernel handles both; the packed split-bf16 kernel does not
 static bool lin_fwd_fast_ok(const float* x, int x_row, const float* y, int y_row,
-                            const eelg_lin_desc* desc) {
+                            const eelg_lin_desc* desc, bool partial = false) {
   if ((x_row & 3) || (reinterpret_cast<uintptr_t>(x) & 15) || (y_row & 3) ||
       (reinterpret_cast<uintptr_t>(y) & 15))
     return false;
   for (int s = 0; s < desc->n_slots; ++s) {
     const eelg_lin_slot& sl = desc->slot[s];
-    if (sl.n_out % 32 || (sl.y_off & 3) || sl.n_src == 0) return false;   // sourceless: general path writes zeros
+    if ((sl.n_out % (partial ? 4 : 32)) || (sl.y_off & 3) || sl.n_src == 0) return false;   // sourceless: general path writes zeros
     if (sl.d != 1 && sl.d != 3 && sl.d != 5 && sl.d != 7 && sl.d != 9) return false;
     int kt = 0;
     for (int t = 0; t < sl.n_src; ++t) {
-      if (sl.src[t].k % 32 || (sl.src[t].x_off & 3)) return false;
-      kt += sl.src[t].k;
+      const bool kpart = partial && sl.n_src == 1 && sl.src[t].k % 4 == 0;
+      if ((sl.src[t].k % 32 && !kpart) || (sl.src[t].x_off & 3)) return false;
+      kt += (sl.src[t].k + 31) / 32 * 32;
     }
     if (kt > LINF_KMAX) return false;
   }

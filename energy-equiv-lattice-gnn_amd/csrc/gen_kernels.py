@@ -706,8 +706,7 @@ def _emit_tp_bwf(name, sfx, bgroups, paths, target, din, nshp, wn, node_off, bf,
                 f"  {{ const float* __restrict__ gp = gy + (size_t)(n0 + ({pre}ok ? {pre}r : 0)) * {tdim} + {pre}tk.gyoff + {pre}m + hf * 16 * {pre}tk.d3;",
                 f"    const eelg_f4a* __restrict__ wp = reinterpret_cast<const eelg_f4a*>(wl + {pre}tk.woff + u * 32 + hf * 16);",
                 f"    {pre}a0 = wp[0]; {pre}a1 = wp[1]; {pre}a2 = wp[2]; {pre}a3 = wp[3];",
-                "#pragma unroll",
-                f"    for (int st = 0; st < 16; ++st) {pre}b[st] = {pre}ok ? gp[st * {pre}tk.d3] : 0.0f; }}"]
+                "    " + " ".join(f"{pre}b[{st}] = {pre}ok ? gp[{st} * {pre}tk.d3] : 0.0f;" for st in range(16)) + " }"]
     if P1:
         L.append("  if (t < t1) {")
         L += ["  " + ln for ln in p1_load("", "t")]
@@ -721,15 +720,14 @@ def _emit_tp_bwf(name, sfx, bgroups, paths, target, din, nshp, wn, node_off, bf,
         L.append(f"    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a{st // 4}[{st % 4}], b[{st}], acc, 0, 0, 0);")
     L.append("    if (ok) {")
     L.append("      float* __restrict__ gd = Gs + r * sg + tk.lds + 4 * hf * tk.d3 + m;")
-    L.append("#pragma unroll")
-    L.append("      for (int v = 0; v < 16; ++v) gd[((v & 3) + 8 * (v >> 2)) * tk.d3] = acc[v] * tk.alpha;")
+    L += ["      " + " ".join(f"gd[{(v & 3) + 8 * (v >> 2)} * tk.d3] = acc[{v}] * tk.alpha;" for v in range(v0, v0 + 4))
+          for v0 in range(0, 16, 4)]
     L.append("    }")
     if P1:
         L.append("    t += 4;")
         L.append("    if (t >= t1) break;")
         L.append("    tk = ntk; col = ncol; r = nr; m = nm; ok = nok; a0 = na0; a1 = na1; a2 = na2; a3 = na3;")
-        L.append("#pragma unroll")
-        L.append("    for (int st = 0; st < 16; ++st) b[st] = nb[st];")
+        L.append("    " + " ".join(f"b[{st}] = nb[{st}];" for st in range(16)))
         L.append("  }}")
     else:
         L.append("  }")

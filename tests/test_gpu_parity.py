@@ -266,6 +266,11 @@ def test_model_batching_and_permutation_invariance():
     ("32x0e+32x1o+32x2e+32x3o+32x4e", "160x0e+32x1o+32x2e+32x3o+32x4e", False, 257),
     ("16x0e+16x1o+16x2e+16x3o+16x4e", "2x0e+2x2e+1x4e", True, 5),
     ("32x0e+16x0e+32x1o", "32x0e+32x1o+8x2e", True, 70),   # fan-in of 2 sources, empty slot
+    # fast kernel with partial tiles: the readout's 32 -> 16 channels (its grad-x: a 16-wide K
+    # chunk), a second partial column tile, single-source K of 48 and 12
+    ("32x0e+32x1o+32x2e+32x3o+32x4e", "16x0e+16x1o+16x2e+16x3o+16x4e", True, 1000),
+    ("32x0e+32x1o", "48x0e+20x1o", True, 333),
+    ("12x0e+40x1o+48x2e", "32x0e+32x1o+64x2e", False, 77),
 ])
 def test_irreps_linear_fwd_bwd(irreps_in, irreps_out, bias, n):
     from gnn.o3 import Linear

@@ -179,7 +179,8 @@ def main():
         ops._lib.check(lib.eelg_sc_bwd_coef(sidx, ops._lib.ptr(xt), ops._lib.ptr(gt), n, 32, chunk,
                                             ops._lib.ptr(part), ops._lib.stream(x)), "bc")
     rec("sc_bwd_coef", timeit_if("sc_bwd_coef", scbc, args.reps), None, 2 * n * 32 * (nt + 3250))
-    for name, ii, oo in [("lin 800->800", hid, hid),
+    for name, ii, oo in [("lin 800->400 (readout, 16 ch)", hid, "16x0e+16x1o+16x2e+16x3o+16x4e"),
+                         ("lin 800->800", hid, hid),
                          ("lin 7360->800", "160x0e+256x1o+320x2e+320x3o+288x4e", hid)]:
         lin = Linear(ii, oo).to(dev)
         xi = torch.randn(n, lin.irreps_in.dim, device=dev)
