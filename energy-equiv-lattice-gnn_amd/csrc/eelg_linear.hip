@@ -510,9 +510,11 @@ static bool lin_bwdw_fast_ok(const float* x, int x_row, const float* g, int g_ro
 #endif
 #define LINF_KMAX 320          // sum of the slot's source K held in LDS
 // the fast kernel also takes partial column tiles / a partial single-source K chunk (the readout
-// tail's 32 -> 16-channel linear and its grad-x; they ran on lin_fwd_kernel at ~70 us each)
+// tail's 32 -> 16-channel linear and its grad-x: lin_fwd_kernel ~0.072 ms each, partial fast
+// path 0.047 ms, kbench r09k; parity r09k).  Off by default at the end of round 6: the 16-channel
+// model suite (tests/test_gpu_mul.py, where every linear would take it) has not run on it yet
 #ifndef LINF_PARTIAL
-#define LINF_PARTIAL 1
+#define LINF_PARTIAL 0
 #endif
 #define LINF_XW 1152           // per-wave X region (floats) >= NB * SX for every D
 
