@@ -407,20 +407,16 @@ def _tp_fwd(x, sh, w, csr: EdgeCSR, cfg: int, info: Dict[str, int], inv_norm: fl
     return agg, x, sh, w
 
 
-_BWF_OK: Dict[tuple, bool] = {}
-
-
 def tp_linear_fusable(cfg: int, lin, paths) -> bool:
     """whether ``eelg_tp_bwd_fused`` serves ``lin(tp_interaction(...))`` for TP config ``cfg``:
     generated for it (mul 32), and its slot table (weight offset, alpha, gy offset per TP slot)
     equals what ``lin`` (an ``o3.Linear`` over the TP's output irreps) computes.  ``paths``:
-    ``cg.tp_paths`` of the block (slot, l3, out_off).  Cached per (cfg, linear)."""
-    key = (cfg, id(lin))
-    if key in _BWF_OK:
-        return _BWF_OK[key]
-    ok = _bwf_table_matches(cfg, lin, paths)
-    _BWF_OK[key] = ok
-    return ok
+    ``cg.tp_paths`` of the block (slot, l3, out_off).  Cached on the linear, per config (not by
+    ``id()``: a freed linear's id can be reused by a new one)."""
+    cache = lin.__dict__.setdefault("_bwf_ok", {})
+    if cfg not in cache:
+        cache[cfg] = _bwf_table_matches(cfg, lin, paths)
+    return cache[cfg]
 
 
 def _bwf_table_matches(cfg: int, lin, paths) -> bool:
