@@ -511,8 +511,8 @@ static bool lin_bwdw_fast_ok(const float* x, int x_row, const float* g, int g_ro
 #define LINF_KMAX 320          // sum of the slot's source K held in LDS
 // the fast kernel also takes partial column tiles / a partial single-source K chunk (the readout
 // tail's 32 -> 16-channel linear and its grad-x: lin_fwd_kernel ~0.072 ms each, partial fast
-// path 0.047 ms, kbench r09k; parity r09k).  Off by default at the end of round 6: the 16-channel
-// model suite (tests/test_gpu_mul.py, where every linear would take it) has not run on it yet
+// path 0.047 ms, kbench r09k; parity r09k / r09l incl. the 16-channel suite).  Off by default:
+// no step gain (r09l alternating: off 2209.7 / 2186.0, on 2201.4 / 2120.4 graphs/s)
 #ifndef LINF_PARTIAL
 #define LINF_PARTIAL 0
 #endif
